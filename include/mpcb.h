@@ -1,0 +1,150 @@
+/*
+ * mpcb.h — C ABI of libmpcblaster.so, the MI355X-native batched MPC hot path.
+ *
+ * Drop-in boundary for the per-control-step solve of sml93/mpc_blaster.  The reference crosses
+ * this boundary once per control step at ``ocp_solver.solve()``
+ * (src/scripts/simulation_blaster.py:80, mavros_blaster_sim.py:85), i.e. acados'
+ * AcadosOcpSolver over its ctypes-loaded generated library; the plant step is
+ * ``integrator.solve()`` (simulation_blaster.py:94-104, AcadosSimSolver).  Each entry point
+ * below names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Plain C: pointers + sizes, no C++ or torch types.  Every call returns 0 or a negative
+ *    MPCB_E_* code; ``mpcb_last_error()`` gives a thread-local message.
+ *  - Array arguments are DEVICE pointers (HBM, caller-owned, e.g. torch ROCm tensors) of the
+ *    handle's dtype (double when cfg.dtype == MPCB_F64, float when MPCB_F32).  Per-instance
+ *    strides are in ELEMENTS; a stride of 0 broadcasts one array to the whole batch.
+ *  - Calls are asynchronous on ``hip_stream`` (NULL = default stream).  The Python facade
+ *    synchronises to keep acados' synchronous semantics.
+ *  - A handle is bound to one device, owns its workspace, and is not re-entrant.
+ *  - Per-instance ``status`` (acados codes: 0 success, 1 NaN detected, 2 max iterations,
+ *    4 QP failure) is separate from the call-level return code.
+ */
+#ifndef MPCB_H
+#define MPCB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCB_ABI_VERSION 1
+
+enum { MPCB_F64 = 0, MPCB_F32 = 1 };
+enum { MPCB_MODE_ROLLOUT = 0, MPCB_MODE_ITERATE = 1 };
+enum {
+  MPCB_OK = 0,
+  MPCB_E_INVALID = -1,   /* bad argument / shape */
+  MPCB_E_HIP = -2,       /* HIP runtime error */
+  MPCB_E_NOMEM = -3,     /* workspace allocation failed */
+  MPCB_E_UNSUPPORTED = -4
+};
+enum { MPCB_STATUS_OK = 0, MPCB_STATUS_NAN = 1, MPCB_STATUS_MAXITER = 2, MPCB_STATUS_QP_FAIL = 4 };
+
+#define MPCB_MAX_NX 17
+#define MPCB_MAX_NU 6
+
+/*
+ * Problem definition: replaces the ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t,
+ * blastThruster, statesBound, controlBound)`` constructor + ``generateController()``
+ * (src/scripts/blastermodel.py:16, :214-292) that build the acados OCP.
+ * Matrices are row-major, leading dimension nx (Q, QN) or nu (R).
+ */
+typedef struct mpcb_config {
+  int32_t nx;            /* 12 (rigid-body slice); 17 reserved for the full model */
+  int32_t nu;            /* 4 */
+  int32_t N;             /* horizon (ocp.dims.N, blastermodel.py:226) */
+  int32_t dtype;         /* MPCB_F64 | MPCB_F32 */
+  int32_t box_u;         /* 1: lbu <= u <= ubu on stages 0..N-1 (idxbu, blastermodel.py:261) */
+  int32_t max_as_iter;   /* active-set iteration cap for box_u */
+  int32_t reserved[2];
+  double dt;             /* Tf / N (solver_options.tf, blastermodel.py:287) */
+  double cost_scale;     /* stage-cost scaling; acados uses time_steps[k] = dt */
+  double mass, lx, ly, c, g, t_blast;
+  double J[9];           /* inertia (row-major 3x3) */
+  double Q[MPCB_MAX_NX * MPCB_MAX_NX];   /* stage state weight  (W[:nx,:nx]) */
+  double R[MPCB_MAX_NU * MPCB_MAX_NU];   /* stage input weight  (W[nx:,nx:]) */
+  double QN[MPCB_MAX_NX * MPCB_MAX_NX];  /* terminal weight (W_e = Q_t) */
+  double lbu[MPCB_MAX_NU], ubu[MPCB_MAX_NU];
+} mpcb_config;
+
+typedef struct mpcb_handle mpcb_handle;
+
+/* Library / device lifetime.  Replaces AcadosOcpSolver(ocp, json_file) construction
+ * (blastermodel.py:289): validates the config, uploads weights, sizes the workspace. */
+int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out);
+int mpcb_destroy(mpcb_handle* h);
+const char* mpcb_last_error(void);
+int mpcb_abi_version(void);
+/* Number of instances currently processed concurrently per launch (informational). */
+int64_t mpcb_workspace_bytes(const mpcb_handle* h);
+
+/*
+ * One SQP_RTI step for B independent instances, linearised at the RK4 rollout of u_ref from
+ * x0 (north_star surface ``solve(x0, x_ref, u_ref)``).  Replaces, per instance, the call
+ * sequence ocp_solver.set(0,'lbx'/'ubx',x0) / cost_set(k,'yref',...) / solve() /
+ * get(0,'u') / get(k,'x') (simulation_blaster.py:60-89).
+ *   x0    [B, nx]            stride x0_sb
+ *   xref  [B|1, N+1, nx]     stride xref_sb (0 = broadcast)
+ *   uref  [B|1, N, nu]       stride uref_sb
+ *   wind  [B|1, 3] or NULL   world-frame disturbance force (build extension, c5)
+ *   u0    [B, nu]            first-step control u0* (required)
+ *   X     [B, N+1, nx]|NULL  predicted state trajectory xbar + dx (linear prediction)
+ *   U     [B, N, nu]|NULL    predicted controls
+ *   status[B] int32          per-instance status
+ */
+int mpcb_solve(mpcb_handle* h, int64_t B,
+               const void* x0, int64_t x0_sb,
+               const void* xref, int64_t xref_sb,
+               const void* uref, int64_t uref_sb,
+               const void* wind, int64_t wind_sb,
+               void* u0, void* X, void* U, int32_t* status, void* hip_stream);
+
+/*
+ * acados SQP_RTI semantics: linearise at the persistent iterate (xbar [B,N+1,nx],
+ * ubar [B,N,nu]) with gaps, x0 enforced through dx_0 = x0 - xbar_0; outputs the full-step
+ * iterate X = xbar + dx, U = ubar + du (X/U may alias xbar/ubar).  This is what one
+ * ``ocp_solver.solve()`` does on the persistent solver object (simulation_blaster.py:80).
+ */
+int mpcb_solve_iterate(mpcb_handle* h, int64_t B,
+                       const void* x0, int64_t x0_sb,
+                       const void* xbar, const void* ubar,
+                       const void* xref, int64_t xref_sb,
+                       const void* uref, int64_t uref_sb,
+                       const void* wind, int64_t wind_sb,
+                       void* u0, void* X, void* U, int32_t* status, void* hip_stream);
+
+/*
+ * Linearisation only (debug / parity): RK4 + exact forward sensitivities of every shooting
+ * interval.  A [B,N,nx,nx], Bm [B,N,nx,nu], xnext [B,N,nx] = Phi(xbar_k, ubar_k).
+ * Replaces acados sim_erk with sens_forward (what SQP_RTI evaluates inside solve()).
+ */
+int mpcb_linearize(mpcb_handle* h, int64_t B, const void* xbar, const void* ubar,
+                   const void* wind, int64_t wind_sb,
+                   void* A, void* Bm, void* xnext, void* hip_stream);
+
+/*
+ * Plant integrator: x_out[b] = Phi(x[b], u[b]) with step T (one RK4 step).  Replaces
+ * AcadosSimSolver set('x')/set('u')/solve()/get('x') (simulation_blaster.py:94-104).
+ */
+int mpcb_sim_step(mpcb_handle* h, int64_t B, const void* x, const void* u, const void* wind,
+                  int64_t wind_sb, double T, void* x_out, void* hip_stream);
+
+/*
+ * Synthetic inputs (SURVEY §8 d): Philox4x32-10 keyed by (seed, id_offset + i).
+ *   ref_kind 0 = hover reference, 1 = per-instance sinusoid (c3);  wind may be NULL.
+ * Writes x0 [B,nx], xref [B,N+1,nx] (or [1,...] if ref_kind==0 and xref_sb==0), uref likewise.
+ */
+int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_t id_offset, int ref_kind,
+                    void* x0, void* xref, int64_t xref_sb, void* uref, int64_t uref_sb,
+                    void* wind, void* hip_stream);
+
+/* Histogram of u0 per input channel over [lo, hi) into counts[nu][nbins] (int64, accumulated). */
+int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,
+                   int64_t* counts, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCB_H */

@@ -1,0 +1,222 @@
+"""Batch API over the HIP library: ``solve(x0, x_ref, u_ref)`` / ``get_control()``.
+
+This is the north_star call surface for the per-control-step solve that the reference runs
+one instance at a time through ``ocp_solver.solve()`` (src/scripts/simulation_blaster.py:80).
+Device buffers are torch ROCm tensors (plumbing only); every computation runs in
+libmpcblaster.so.  Calls are asynchronous on torch's current stream; results are valid once
+that stream is synchronised (``torch.cuda.synchronize()`` or reading them on the host).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .config import NU, NX, MPCConfig
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class BatchedMPC:
+    """A handle bound to one GPU holding the workspace for up to ``max_batch`` instances."""
+
+    def __init__(self, config: MPCConfig, max_batch: int, device: int | None = None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError('BatchedMPC needs a ROCm GPU (torch.cuda.is_available() is False)')
+        self.lib = _lib.load()
+        self.cfg = config
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.max_batch = int(max_batch)
+        self._c = config.to_c()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.mpcb_create(ctypes.byref(self._c), self.device, self.max_batch,
+                                            ctypes.byref(h)))
+        self._h = h
+        self.dtype = config.torch_dtype
+        self._u0 = self._X = self._U = self._status = None
+
+    # ------------------------------------------------------------------ helpers
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            self.lib.mpcb_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def workspace_bytes(self) -> int:
+        return int(self.lib.mpcb_workspace_bytes(self._h))
+
+    def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):
+        """Coerce to a contiguous device tensor of the handle dtype; return (tensor, stride)."""
+        torch = _torch()
+        t = torch.as_tensor(t, dtype=self.dtype, device=f'cuda:{self.device}')
+        if t.dim() == len(shape_tail):
+            t = t.unsqueeze(0)
+        if tuple(t.shape[1:]) != tuple(shape_tail):
+            raise ValueError(f'{name}: expected shape [B, {", ".join(map(str, shape_tail))}], '
+                             f'got {tuple(t.shape)}')
+        t = t.contiguous()
+        n = int(np.prod(shape_tail))
+        if batch is not None and t.shape[0] != batch:
+            if allow_broadcast and t.shape[0] == 1:
+                return t, 0
+            raise ValueError(f'{name}: batch {t.shape[0]} != {batch}')
+        return t, n
+
+    def _stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def _outputs(self, B, want_traj):
+        torch = _torch()
+        dev = f'cuda:{self.device}'
+        N = self.cfg.N
+        self._u0 = torch.empty((B, NU), dtype=self.dtype, device=dev)
+        self._status = torch.empty((B,), dtype=torch.int32, device=dev)
+        if want_traj:
+            self._X = torch.empty((B, N + 1, NX), dtype=self.dtype, device=dev)
+            self._U = torch.empty((B, N, NU), dtype=self.dtype, device=dev)
+        else:
+            self._X = self._U = None
+
+    @staticmethod
+    def _ptr(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+    # ------------------------------------------------------------------ API
+    def solve(self, x0, x_ref, u_ref, wind=None, want_traj: bool = True, out=None):
+        """One SQP_RTI step per instance, linearised at the RK4 rollout of u_ref from x0.
+
+        x0 [B,12]; x_ref [B|1,N+1,12]; u_ref [B|1,N,4]; wind [B|1,3] (optional).
+        Returns the first-step controls u0* [B,4] (device tensor, async).
+        """
+        N = self.cfg.N
+        x0, _ = self._dev(x0, (NX,), 'x0')
+        B = x0.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f'batch {B} > max_batch {self.max_batch}')
+        xr, xr_sb = self._dev(x_ref, (N + 1, NX), 'x_ref', B, allow_broadcast=True)
+        ur, ur_sb = self._dev(u_ref, (N, NU), 'u_ref', B, allow_broadcast=True)
+        wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
+        if out is None:
+            self._outputs(B, want_traj)
+        else:
+            self._u0, self._X, self._U, self._status = out
+        self._keep = (x0, xr, ur, wd)
+        _lib.check(self.lib.mpcb_solve(
+            self._h, B, self._ptr(x0), NX, self._ptr(xr), xr_sb, self._ptr(ur), ur_sb,
+            self._ptr(wd), wd_sb, self._ptr(self._u0), self._ptr(self._X), self._ptr(self._U),
+            self._ptr(self._status), self._stream()))
+        return self._u0
+
+    def solve_iterate(self, x0, xbar, ubar, x_ref, u_ref, wind=None, out=None):
+        """acados SQP_RTI step from the persistent iterate (xbar [B,N+1,12], ubar [B,N,4])."""
+        N = self.cfg.N
+        x0, _ = self._dev(x0, (NX,), 'x0')
+        B = x0.shape[0]
+        xb, _ = self._dev(xbar, (N + 1, NX), 'xbar', B)
+        ub, _ = self._dev(ubar, (N, NU), 'ubar', B)
+        xr, xr_sb = self._dev(x_ref, (N + 1, NX), 'x_ref', B, allow_broadcast=True)
+        ur, ur_sb = self._dev(u_ref, (N, NU), 'u_ref', B, allow_broadcast=True)
+        wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
+        if out is None:
+            self._outputs(B, True)
+        else:
+            self._u0, self._X, self._U, self._status = out
+        self._keep = (x0, xb, ub, xr, ur, wd)
+        _lib.check(self.lib.mpcb_solve_iterate(
+            self._h, B, self._ptr(x0), NX, self._ptr(xb), self._ptr(ub), self._ptr(xr), xr_sb,
+            self._ptr(ur), ur_sb, self._ptr(wd), wd_sb, self._ptr(self._u0), self._ptr(self._X),
+            self._ptr(self._U), self._ptr(self._status), self._stream()))
+        return self._u0
+
+    def get_control(self):
+        """First-step control u0* of the last solve, [B,4] device tensor."""
+        if self._u0 is None:
+            raise RuntimeError('solve() has not been called')
+        return self._u0
+
+    def get_state_trajectory(self):
+        """Predicted state trajectory X = xbar + dx of the last solve, [B,N+1,12]."""
+        if self._X is None:
+            raise RuntimeError('no trajectory: call solve(..., want_traj=True)')
+        return self._X
+
+    def get_input_trajectory(self):
+        if self._U is None:
+            raise RuntimeError('no trajectory: call solve(..., want_traj=True)')
+        return self._U
+
+    def get_status(self):
+        return self._status
+
+    def linearize(self, xbar, ubar, wind=None):
+        """A [B,N,12,12], B [B,N,12,4], Phi(xbar_k, ubar_k) [B,N,12] (debug / parity)."""
+        torch = _torch()
+        N = self.cfg.N
+        xb, _ = self._dev(xbar, (N + 1, NX), 'xbar')
+        B = xb.shape[0]
+        ub, _ = self._dev(ubar, (N, NU), 'ubar', B)
+        wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
+        dev = f'cuda:{self.device}'
+        A = torch.empty((B, N, NX, NX), dtype=self.dtype, device=dev)
+        Bm = torch.empty((B, N, NX, NU), dtype=self.dtype, device=dev)
+        xn = torch.empty((B, N, NX), dtype=self.dtype, device=dev)
+        _lib.check(self.lib.mpcb_linearize(self._h, B, self._ptr(xb), self._ptr(ub), self._ptr(wd),
+                                           wd_sb, self._ptr(A), self._ptr(Bm), self._ptr(xn),
+                                           self._stream()))
+        self._keep = (xb, ub, wd)
+        return A, Bm, xn
+
+    def sim_step(self, x, u, T=None, wind=None):
+        """Plant integrator: one RK4 step of length T (default dt) — AcadosSimSolver.solve()."""
+        torch = _torch()
+        xs, _ = self._dev(x, (NX,), 'x')
+        B = xs.shape[0]
+        us, _ = self._dev(u, (NU,), 'u', B)
+        wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
+        xo = torch.empty_like(xs)
+        _lib.check(self.lib.mpcb_sim_step(self._h, B, self._ptr(xs), self._ptr(us), self._ptr(wd),
+                                          wd_sb, float(self.cfg.dt if T is None else T),
+                                          self._ptr(xo), self._stream()))
+        self._keep = (xs, us, wd)
+        return xo
+
+    def gen_inputs(self, B, seed, id_offset=0, ref='hover', wind=False):
+        """Synthetic inputs on device (SURVEY §8 d): x0 [B,12], x_ref, u_ref (broadcast for hover)."""
+        torch = _torch()
+        N = self.cfg.N
+        dev = f'cuda:{self.device}'
+        x0 = torch.empty((B, NX), dtype=self.dtype, device=dev)
+        if ref == 'sine':
+            xr = torch.empty((B, N + 1, NX), dtype=self.dtype, device=dev)
+            xr_sb, kind = (N + 1) * NX, 1
+        else:
+            xr = torch.empty((1, N + 1, NX), dtype=self.dtype, device=dev)
+            xr_sb, kind = 0, 0
+        ur = torch.empty((1, N, NU), dtype=self.dtype, device=dev)
+        wd = torch.empty((B, 3), dtype=self.dtype, device=dev) if wind else None
+        _lib.check(self.lib.mpcb_gen_inputs(self._h, B, int(seed), int(id_offset), kind,
+                                            self._ptr(x0), self._ptr(xr), xr_sb, self._ptr(ur), 0,
+                                            self._ptr(wd), self._stream()))
+        return dict(x0=x0, xref=xr, uref=ur, wind=wd)
+
+    def histogram(self, u0, lo=0.0, hi=65.0, nbins=64, counts=None):
+        """Accumulate a per-motor histogram of u0 into int64 counts [4, nbins] (device)."""
+        torch = _torch()
+        u, _ = self._dev(u0, (NU,), 'u0')
+        if counts is None:
+            counts = torch.zeros((NU, nbins), dtype=torch.int64, device=f'cuda:{self.device}')
+        _lib.check(self.lib.mpcb_histogram(self._h, u.shape[0], self._ptr(u), float(lo), float(hi),
+                                           int(nbins), self._ptr(counts), self._stream()))
+        return counts

@@ -1,0 +1,43 @@
+"""Build libmpcblaster.so in-tree with hipcc for gfx950 (no JIT cache, no site-packages)."""
+from __future__ import annotations
+
+import os
+import shlex
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+SOURCES = ['mpcb_solve.hip', 'mpcb_aux.hip', 'mpcb_capi.hip']
+OUT = os.path.join(HERE, 'libmpcblaster.so')
+ARCH = os.environ.get('MPCB_OFFLOAD_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', f'--offload-arch={ARCH}',
+         '-Wall', '-Wno-unused-result', '-Wno-unused-variable']
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    deps.append(os.path.join(os.path.dirname(HERE), 'include', 'mpcb.h'))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return OUT
+    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', OUT + '.tmp']
+    if verbose:
+        print('[mpcb build]', ' '.join(shlex.quote(c) for c in cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f'hipcc failed ({r.returncode})')
+    os.replace(OUT + '.tmp', OUT)
+    return OUT
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv)

@@ -1,0 +1,318 @@
+// mpcb_capi.hip — extern "C" boundary of libmpcblaster.so (declared in include/mpcb.h).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/mpcb.h"
+#include "mpcb_kernels.h"
+
+using namespace mpcb;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess) return fail(MPCB_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+bool inv3(const double* A, double* out) {
+  const double d = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
+                   A[2] * (A[3] * A[7] - A[4] * A[6]);
+  if (!(std::fabs(d) > 0)) return false;
+  out[0] = (A[4] * A[8] - A[5] * A[7]) / d;
+  out[1] = (A[2] * A[7] - A[1] * A[8]) / d;
+  out[2] = (A[1] * A[5] - A[2] * A[4]) / d;
+  out[3] = (A[5] * A[6] - A[3] * A[8]) / d;
+  out[4] = (A[0] * A[8] - A[2] * A[6]) / d;
+  out[5] = (A[2] * A[3] - A[0] * A[5]) / d;
+  out[6] = (A[3] * A[7] - A[4] * A[6]) / d;
+  out[7] = (A[1] * A[6] - A[0] * A[7]) / d;
+  out[8] = (A[0] * A[4] - A[1] * A[3]) / d;
+  return true;
+}
+}  // namespace
+
+struct mpcb_handle {
+  mpcb_config cfg;
+  int device;
+  int64_t max_batch;
+  int grid;              // resident slots (one wavefront of GROUPS instances each)
+  void* weights;         // Weights<T>
+  void* scratch;
+  int64_t slot_elems;
+  int64_t scratch_bytes;
+  Model<double> Md;
+  Model<float> Mf;
+};
+
+extern "C" const char* mpcb_last_error(void) { return g_err.c_str(); }
+extern "C" int mpcb_abi_version(void) { return MPCB_ABI_VERSION; }
+
+extern "C" int64_t mpcb_workspace_bytes(const mpcb_handle* h) { return h ? h->scratch_bytes : 0; }
+
+template <class T>
+static void fill_weights(const mpcb_config& c, Weights<T>& w) {
+  for (int i = 0; i < NX * NX; ++i) {
+    w.Q[i] = (T)c.Q[i];
+    w.QN[i] = (T)c.QN[i];
+  }
+  for (int i = 0; i < NU * NU; ++i) w.R[i] = (T)c.R[i];
+  for (int i = 0; i < NU; ++i) {
+    w.lbu[i] = (T)c.lbu[i];
+    w.ubu[i] = (T)c.ubu[i];
+  }
+}
+
+template <class T>
+static void fill_model(const mpcb_config& c, const double* Jinv, Model<T>& M) {
+  M.minv = (T)(1.0 / c.mass);
+  M.g = (T)c.g;
+  M.t_blast = (T)c.t_blast;
+  M.lx = (T)c.lx;
+  M.ly = (T)c.ly;
+  M.c = (T)c.c;
+  for (int i = 0; i < 9; ++i) {
+    M.J[i] = (T)c.J[i];
+    M.Jinv[i] = (T)Jinv[i];
+  }
+}
+
+extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
+  if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");
+  *out = nullptr;
+  if (cfg->nx != NX || cfg->nu != NU)
+    return fail(MPCB_E_UNSUPPORTED, "nx=%d nu=%d: this build implements the 12-state/4-input model",
+                cfg->nx, cfg->nu);
+  if (cfg->N < 1 || cfg->N > 4096) return fail(MPCB_E_INVALID, "horizon N=%d out of range", cfg->N);
+  if (cfg->box_u && cfg->N > 64) return fail(MPCB_E_UNSUPPORTED, "box_u needs N <= 64 (N=%d)", cfg->N);
+  if (cfg->dtype != MPCB_F64 && cfg->dtype != MPCB_F32)
+    return fail(MPCB_E_INVALID, "dtype=%d", cfg->dtype);
+  if (!(cfg->dt > 0) || !(cfg->mass > 0)) return fail(MPCB_E_INVALID, "dt and mass must be > 0");
+  if (max_batch < 1) return fail(MPCB_E_INVALID, "max_batch=%lld", (long long)max_batch);
+  if (cfg->box_u && cfg->max_as_iter < 1) return fail(MPCB_E_INVALID, "max_as_iter must be >= 1");
+  double Jinv[9];
+  if (!inv3(cfg->J, Jinv)) return fail(MPCB_E_INVALID, "inertia J is singular");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MPCB_E_INVALID, "device %d of %d", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+
+  mpcb_handle* h = new mpcb_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  h->max_batch = max_batch;
+  const bool f64 = cfg->dtype == MPCB_F64;
+  // resident slots: one 64-thread workgroup per slot, a few per SIMD
+  const int64_t waves_needed = (max_batch + GROUPS - 1) / GROUPS;
+  int64_t grid = (int64_t)prop.multiProcessorCount * 16;
+  if (grid > waves_needed) grid = waves_needed;
+  h->grid = (int)grid;
+  h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
+  const size_t esz = f64 ? sizeof(double) : sizeof(float);
+  h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
+  fill_model(*cfg, Jinv, h->Md);
+  fill_model(*cfg, Jinv, h->Mf);
+  hipError_t e = hipMalloc(&h->scratch, (size_t)h->scratch_bytes);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(MPCB_E_NOMEM, "workspace %lld bytes: %s", (long long)h->scratch_bytes, hipGetErrorString(e));
+  }
+  const size_t wbytes = f64 ? sizeof(Weights<double>) : sizeof(Weights<float>);
+  e = hipMalloc(&h->weights, wbytes);
+  if (e != hipSuccess) {
+    (void)hipFree(h->scratch);
+    delete h;
+    return fail(MPCB_E_NOMEM, "weights: %s", hipGetErrorString(e));
+  }
+  if (f64) {
+    Weights<double> w;
+    fill_weights(*cfg, w);
+    e = hipMemcpy(h->weights, &w, sizeof(w), hipMemcpyHostToDevice);
+  } else {
+    Weights<float> w;
+    fill_weights(*cfg, w);
+    e = hipMemcpy(h->weights, &w, sizeof(w), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    (void)hipFree(h->scratch);
+    (void)hipFree(h->weights);
+    delete h;
+    return fail(MPCB_E_HIP, "weights upload: %s", hipGetErrorString(e));
+  }
+  *out = h;
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_destroy(mpcb_handle* h) {
+  if (!h) return MPCB_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->scratch);
+  (void)hipFree(h->weights);
+  delete h;
+  return MPCB_OK;
+}
+
+template <class T>
+static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64_t x0_sb,
+                      const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
+                      const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
+                      void* u0, void* X, void* U, int32_t* status, void* stream) {
+  SolveArgs<T> a;
+  a.B = B;
+  a.N = h->cfg.N;
+  a.mode = mode;
+  a.box = h->cfg.box_u;
+  a.max_as_iter = h->cfg.max_as_iter;
+  a.h = (T)h->cfg.dt;
+  a.s = (T)h->cfg.cost_scale;
+  if constexpr (sizeof(T) == 8) a.M = h->Md; else a.M = h->Mf;
+  a.W = reinterpret_cast<const Weights<T>*>(h->weights);
+  a.x0 = (const T*)x0; a.x0_sb = x0_sb;
+  a.xref = (const T*)xref; a.xref_sb = xref_sb;
+  a.uref = (const T*)uref; a.uref_sb = uref_sb;
+  a.wind = (const T*)wind; a.wind_sb = wind_sb;
+  a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
+  a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
+  a.scratch = (T*)h->scratch;
+  a.slot_elems = h->slot_elems;
+  const int64_t waves = (B + GROUPS - 1) / GROUPS;
+  const int grid = (int)(waves < h->grid ? waves : h->grid);
+  hipError_t e = launch_solve<T>(a, grid, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "solve launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}
+
+static int check_solve(mpcb_handle* h, int64_t B, const void* x0, const void* xref, const void* uref,
+                       const void* u0, const int32_t* status) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (B < 0 || B > h->max_batch)
+    return fail(MPCB_E_INVALID, "batch %lld exceeds max_batch %lld", (long long)B, (long long)h->max_batch);
+  if (B > 0 && (!x0 || !xref || !uref || !u0 || !status))
+    return fail(MPCB_E_INVALID, "x0, xref, uref, u0 and status are required");
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_solve(mpcb_handle* h, int64_t B, const void* x0, int64_t x0_sb, const void* xref,
+               int64_t xref_sb, const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
+               void* u0, void* X, void* U, int32_t* status, void* stream) {
+  int rc = check_solve(h, B, x0, xref, uref, u0, status);
+  if (rc || B == 0) return rc;
+  HIP_TRY(hipSetDevice(h->device));
+  if (h->cfg.dtype == MPCB_F64)
+    return solve_impl<double>(h, B, MPCB_MODE_ROLLOUT, x0, x0_sb, nullptr, nullptr, xref, xref_sb, uref,
+                              uref_sb, wind, wind_sb, u0, X, U, status, stream);
+  return solve_impl<float>(h, B, MPCB_MODE_ROLLOUT, x0, x0_sb, nullptr, nullptr, xref, xref_sb, uref,
+                           uref_sb, wind, wind_sb, u0, X, U, status, stream);
+}
+
+extern "C" int mpcb_solve_iterate(mpcb_handle* h, int64_t B, const void* x0, int64_t x0_sb, const void* xbar,
+                       const void* ubar, const void* xref, int64_t xref_sb, const void* uref,
+                       int64_t uref_sb, const void* wind, int64_t wind_sb, void* u0, void* X, void* U,
+                       int32_t* status, void* stream) {
+  int rc = check_solve(h, B, x0, xref, uref, u0, status);
+  if (rc || B == 0) return rc;
+  if (!xbar || !ubar) return fail(MPCB_E_INVALID, "xbar and ubar are required");
+  HIP_TRY(hipSetDevice(h->device));
+  if (h->cfg.dtype == MPCB_F64)
+    return solve_impl<double>(h, B, MPCB_MODE_ITERATE, x0, x0_sb, xbar, ubar, xref, xref_sb, uref,
+                              uref_sb, wind, wind_sb, u0, X, U, status, stream);
+  return solve_impl<float>(h, B, MPCB_MODE_ITERATE, x0, x0_sb, xbar, ubar, xref, xref_sb, uref,
+                           uref_sb, wind, wind_sb, u0, X, U, status, stream);
+}
+
+extern "C" int mpcb_linearize(mpcb_handle* h, int64_t B, const void* xbar, const void* ubar, const void* wind,
+                   int64_t wind_sb, void* A, void* Bm, void* xnext, void* stream) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (B < 0) return fail(MPCB_E_INVALID, "negative batch");
+  if (B == 0) return MPCB_OK;
+  if (!xbar || !ubar || !A || !Bm || !xnext) return fail(MPCB_E_INVALID, "null array");
+  HIP_TRY(hipSetDevice(h->device));
+  hipError_t e;
+  if (h->cfg.dtype == MPCB_F64)
+    e = launch_linearize<double>(B, h->cfg.N, h->cfg.dt, h->Md, (const double*)xbar, (const double*)ubar,
+                                 (const double*)wind, wind_sb, (double*)A, (double*)Bm, (double*)xnext,
+                                 (hipStream_t)stream);
+  else
+    e = launch_linearize<float>(B, h->cfg.N, (float)h->cfg.dt, h->Mf, (const float*)xbar, (const float*)ubar,
+                                (const float*)wind, wind_sb, (float*)A, (float*)Bm, (float*)xnext,
+                                (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "linearize launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_sim_step(mpcb_handle* h, int64_t B, const void* x, const void* u, const void* wind,
+                  int64_t wind_sb, double T, void* x_out, void* stream) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (B < 0) return fail(MPCB_E_INVALID, "negative batch");
+  if (B == 0) return MPCB_OK;
+  if (!x || !u || !x_out) return fail(MPCB_E_INVALID, "null array");
+  if (!(T > 0)) return fail(MPCB_E_INVALID, "T must be > 0");
+  HIP_TRY(hipSetDevice(h->device));
+  hipError_t e;
+  if (h->cfg.dtype == MPCB_F64)
+    e = launch_sim_step<double>(B, T, h->Md, (const double*)x, (const double*)u, (const double*)wind,
+                                wind_sb, (double*)x_out, (hipStream_t)stream);
+  else
+    e = launch_sim_step<float>(B, (float)T, h->Mf, (const float*)x, (const float*)u, (const float*)wind,
+                               wind_sb, (float*)x_out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "sim_step launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_t id_offset, int ref_kind, void* x0,
+                    void* xref, int64_t xref_sb, void* uref, int64_t uref_sb, void* wind, void* stream) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (B < 0) return fail(MPCB_E_INVALID, "negative batch");
+  if (B == 0) return MPCB_OK;
+  if (!x0 || !xref || !uref) return fail(MPCB_E_INVALID, "null array");
+  if (ref_kind == 1 && xref_sb == 0) return fail(MPCB_E_INVALID, "sinusoid refs need xref_sb > 0");
+  HIP_TRY(hipSetDevice(h->device));
+  hipError_t e;
+  if (h->cfg.dtype == MPCB_F64)
+    e = launch_gen_inputs<double>(B, h->cfg.N, h->cfg.dt, seed, id_offset, ref_kind, (double*)x0,
+                                  (double*)xref, xref_sb, (double*)uref, uref_sb, (double*)wind,
+                                  (hipStream_t)stream);
+  else
+    e = launch_gen_inputs<float>(B, h->cfg.N, (float)h->cfg.dt, seed, id_offset, ref_kind, (float*)x0,
+                                 (float*)xref, xref_sb, (float*)uref, uref_sb, (float*)wind,
+                                 (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "gen_inputs launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,
+                   int64_t* counts, void* stream) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (B < 0 || nbins < 1 || nbins > 4096 || !(hi > lo)) return fail(MPCB_E_INVALID, "bad histogram args");
+  if (B == 0) return MPCB_OK;
+  if (!u0 || !counts) return fail(MPCB_E_INVALID, "null array");
+  HIP_TRY(hipSetDevice(h->device));
+  hipError_t e;
+  if (h->cfg.dtype == MPCB_F64)
+    e = launch_histogram<double>(B, NU, (const double*)u0, lo, hi, nbins, (unsigned long long*)counts,
+                                 (hipStream_t)stream);
+  else
+    e = launch_histogram<float>(B, NU, (const float*)u0, lo, hi, nbins, (unsigned long long*)counts,
+                                (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "histogram launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}

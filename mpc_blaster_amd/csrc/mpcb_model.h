@@ -1,0 +1,151 @@
+// mpcb_model.h — BLASTER rigid-body dynamics on the device, value + one forward tangent.
+//
+// Restates f_expl_expr of src/scripts/blastermodel.py:95-201 for the 12-state/4-input slice
+// (x = [p, phi, theta, psi, v, omega], u = 4 motor thrusts, swivel alpha = 0 so
+// R_gimbal = I):
+//   p_dot     = v                                              (:124)
+//   eta_dot   = inv(R_to_omega(phi, theta)) @ omega           (:128-141, :162) closed form
+//   v_dot     = (R e3 (sum T) + R e3 T_blast) / m + [0,0,-g]   (:163), R = Rz Ry Rx (:103-122)
+//   omega_dot = inv(J) (M(T) - omega x J omega)               (:95-101, :164)
+// plus an optional world-frame wind force / m in v_dot (c5 build extension).
+//
+// ``f_tan`` evaluates f and its directional derivative J_f(x,u)·(dx,du) in one pass
+// (forward-mode dual numbers).  Each lane of an instance's 16-lane group seeds one
+// direction, so the RK4 sensitivity columns of [A|B] come out one per lane without ever
+// forming the Jacobian (what acados' forward VDE does symbolically).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mpcb {
+
+template <class T>
+struct Model {
+  T minv, g, t_blast, lx, ly, c;
+  T J[9], Jinv[9];
+};
+
+__device__ __forceinline__ void sc(double a, double* s, double* c) { sincos(a, s, c); }
+__device__ __forceinline__ void sc(float a, float* s, float* c) { sincosf(a, s, c); }
+
+// f and (optionally) its tangent.  wind may be nullptr-equivalent (w0=w1=w2=0).
+template <class T, bool TAN>
+__device__ __forceinline__ void f_tan(const T* __restrict__ x, const T* __restrict__ dx,
+                                      const T* __restrict__ u, const T* __restrict__ du,
+                                      const Model<T>& M, const T w[3],
+                                      T* __restrict__ f, T* __restrict__ df) {
+  T sf, cf, st, ct, sp, cp;
+  sc(x[3], &sf, &cf);
+  sc(x[4], &st, &ct);
+  sc(x[5], &sp, &cp);
+  const T ict = T(1) / ct;
+  const T tt = st * ict;
+  const T wx = x[9], wy = x[10], wz = x[11];
+  // ---- p_dot = v
+  f[0] = x[6]; f[1] = x[7]; f[2] = x[8];
+  // ---- eta_dot = W^-1 omega
+  const T a = sf * wy + cf * wz;
+  const T b = cf * wy - sf * wz;
+  f[3] = wx + tt * a;
+  f[4] = b;
+  f[5] = a * ict;
+  // ---- v_dot
+  const T Ttot = (u[0] + u[1]) + (u[2] + u[3]) + M.t_blast;
+  const T s = Ttot * M.minv;
+  const T cfst = cf * st;
+  const T r0 = cp * cfst + sp * sf;
+  const T r1 = sp * cfst - cp * sf;
+  const T r2 = cf * ct;
+  f[6] = r0 * s + w[0] * M.minv;
+  f[7] = r1 * s + w[1] * M.minv;
+  f[8] = r2 * s - M.g + w[2] * M.minv;
+  // ---- omega_dot = Jinv (Mom - w x J w)
+  const T jw0 = M.J[0] * wx + M.J[1] * wy + M.J[2] * wz;
+  const T jw1 = M.J[3] * wx + M.J[4] * wy + M.J[5] * wz;
+  const T jw2 = M.J[6] * wx + M.J[7] * wy + M.J[8] * wz;
+  const T c0 = wy * jw2 - wz * jw1;
+  const T c1 = wz * jw0 - wx * jw2;
+  const T c2 = wx * jw1 - wy * jw0;
+  const T m0 = (u[1] + u[3] - u[0] - u[2]) * M.ly - c0;
+  const T m1 = (u[1] + u[2] - u[0] - u[3]) * M.lx - c1;
+  const T m2 = (u[2] + u[3] - u[0] - u[1]) * M.c - c2;
+  f[9] = M.Jinv[0] * m0 + M.Jinv[1] * m1 + M.Jinv[2] * m2;
+  f[10] = M.Jinv[3] * m0 + M.Jinv[4] * m1 + M.Jinv[5] * m2;
+  f[11] = M.Jinv[6] * m0 + M.Jinv[7] * m1 + M.Jinv[8] * m2;
+  if constexpr (TAN) {
+    const T dphi = dx[3], dth = dx[4], dpsi = dx[5];
+    const T dwx = dx[9], dwy = dx[10], dwz = dx[11];
+    const T dsf = cf * dphi, dcf = -sf * dphi;
+    const T dst = ct * dth, dct = -st * dth;
+    const T dsp = cp * dpsi, dcp = -sp * dpsi;
+    const T dict = -ict * ict * dct;
+    const T dtt = dst * ict + st * dict;
+    df[0] = dx[6]; df[1] = dx[7]; df[2] = dx[8];
+    const T da = dsf * wy + sf * dwy + dcf * wz + cf * dwz;
+    const T db = dcf * wy + cf * dwy - dsf * wz - sf * dwz;
+    df[3] = dwx + dtt * a + tt * da;
+    df[4] = db;
+    df[5] = da * ict + a * dict;
+    const T dT = (du[0] + du[1]) + (du[2] + du[3]);
+    const T ds = dT * M.minv;
+    const T dcfst = dcf * st + cf * dst;
+    const T dr0 = dcp * cfst + cp * dcfst + dsp * sf + sp * dsf;
+    const T dr1 = dsp * cfst + sp * dcfst - dcp * sf - cp * dsf;
+    const T dr2 = dcf * ct + cf * dct;
+    df[6] = dr0 * s + r0 * ds;
+    df[7] = dr1 * s + r1 * ds;
+    df[8] = dr2 * s + r2 * ds;
+    const T djw0 = M.J[0] * dwx + M.J[1] * dwy + M.J[2] * dwz;
+    const T djw1 = M.J[3] * dwx + M.J[4] * dwy + M.J[5] * dwz;
+    const T djw2 = M.J[6] * dwx + M.J[7] * dwy + M.J[8] * dwz;
+    const T dc0 = dwy * jw2 + wy * djw2 - dwz * jw1 - wz * djw1;
+    const T dc1 = dwz * jw0 + wz * djw0 - dwx * jw2 - wx * djw2;
+    const T dc2 = dwx * jw1 + wx * djw1 - dwy * jw0 - wy * djw0;
+    const T dm0 = (du[1] + du[3] - du[0] - du[2]) * M.ly - dc0;
+    const T dm1 = (du[1] + du[2] - du[0] - du[3]) * M.lx - dc1;
+    const T dm2 = (du[2] + du[3] - du[0] - du[1]) * M.c - dc2;
+    df[9] = M.Jinv[0] * dm0 + M.Jinv[1] * dm1 + M.Jinv[2] * dm2;
+    df[10] = M.Jinv[3] * dm0 + M.Jinv[4] * dm1 + M.Jinv[5] * dm2;
+    df[11] = M.Jinv[6] * dm0 + M.Jinv[7] * dm1 + M.Jinv[8] * dm2;
+  }
+}
+
+// One classic RK4 step (acados sim_erk, 4 stages, 1 step) with an optional forward tangent.
+// xn = Phi(x, u); dxn = dPhi/d(x,u) · (dx, du).
+template <class T, bool TAN>
+__device__ __forceinline__ void rk4(const T* __restrict__ x, const T* __restrict__ dx,
+                                    const T* __restrict__ u, const T* __restrict__ du, T h,
+                                    const Model<T>& M, const T w[3], T* __restrict__ xn,
+                                    T* __restrict__ dxn) {
+  constexpr int NX = 12;
+  T k[NX], dk[NX], xs[NX], dxs[NX];
+  const T h2 = T(0.5) * h, h6 = h / T(6);
+  f_tan<T, TAN>(x, dx, u, du, M, w, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    xn[i] = k[i];
+    xs[i] = x[i] + h2 * k[i];
+    if constexpr (TAN) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  }
+  f_tan<T, TAN>(xs, dxs, u, du, M, w, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    xn[i] += T(2) * k[i];
+    xs[i] = x[i] + h2 * k[i];
+    if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  }
+  f_tan<T, TAN>(xs, dxs, u, du, M, w, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    xn[i] += T(2) * k[i];
+    xs[i] = x[i] + h * k[i];
+    if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
+  }
+  f_tan<T, TAN>(xs, dxs, u, du, M, w, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    xn[i] = x[i] + h6 * (xn[i] + k[i]);
+    if constexpr (TAN) dxn[i] = dx[i] + h6 * (dxn[i] + dk[i]);
+  }
+}
+
+}  // namespace mpcb

@@ -1,0 +1,485 @@
+// mpcb_solve.hip — fused batched SQP_RTI step for the BLASTER MPC (gfx950 / MI355X).
+//
+// Replaces, per instance, one acados ``ocp_solver.solve()`` (src/scripts/simulation_blaster.py:80)
+// of the OCP built by blastermodel.py:214-292: ERK4 + forward sensitivities (sim_erk), the
+// Gauss-Newton LINEAR_LS QP, the Riccati-structured QP solve (HPIPM's role), full step.
+//
+// Layout: one wavefront = GROUPS (4) independent instances; an instance owns a 16-lane group and
+// lane j of the group owns DIRECTION j of the 16-dim (x, u) space (j < 12: state, j >= 12: input).
+//  * Pass 1 (forward): nominal RK4 rollout (or copy of the given iterate); every lane of the group
+//    computes the same trajectory, lane j stores component j to the slot workspace.
+//  * Pass 2 (backward Riccati): at stage k lane j integrates RK4 with a forward tangent seeded
+//    by e_j -> column j of [A_k | B_k] lands in lane j without forming any Jacobian.  The value
+//    function P (12x12) and the stage Hessian columns are exchanged through LDS; lane j builds
+//    column j of G = [A|B]^T P [A|B], the 4x4 input block is factorised (Cholesky) redundantly
+//    in every lane, lane j < 12 produces column j of the gain K and of the next P.  Gains go to
+//    the workspace.
+//  * Pass 3 (forward): dx_{k+1} = JVP of RK4 along (dx_k, du_k) (+ gap), du_k = K_k dx_k + kff_k;
+//    writes X = xbar + dx, U = ubar + du.  With input boxes, pass 3 also evaluates the multipliers
+//    and the primal-dual active-set update; passes 2-3 repeat until the active set repeats.
+//
+// HBM traffic per instance is compulsory I/O (x0, refs, u0, X, U) plus the workspace, which is
+// indexed by launch slot (not by instance), so its footprint stays bounded by the resident grid.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcb.h"
+#include "mpcb_kernels.h"
+
+#ifndef MPCB_WAVES
+#define MPCB_WAVES
+#endif
+
+namespace mpcb {
+
+template <class T>
+struct GroupLds {
+  T P[NX * NX];   // value-function Hessian, P[l*NX + i] = column l (symmetric)
+  T X[NZ * NX];   // X[j*NX + i] = ([A|B])_{i j}
+  T Hu[NZ * NU];  // Hu[j*NU + m] = G_{NX+m, j}   (H_ux columns, then H_uu)
+  T v[NZ];        // vector exchange (e = ybar - yref, then pt = p + P b)
+  T hv[NZ];       // gradient h = [h_x; h_u]
+};
+
+// Per-lane record in the workspace, per stage: 4 gain values (+ box-mode extras).
+template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
+
+// Identity that LLVM cannot see through (keeps selects of array elements as selects).
+template <class T> __device__ __forceinline__ T opq(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// a[j] (0 <= j < 16, n <= 16) for a register array, as a bit-tree of selects.  Without the
+// opaque copies InstCombine folds select(load a[i], load a[k]) into a load from a selected
+// address, which turns the register array into a dynamically indexed scratch array.
+template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
+  T l0[8], l1[4], l2[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const T lo = opq(a[(2 * i < n) ? 2 * i : n - 1]);
+    const T hi = opq(a[(2 * i + 1 < n) ? 2 * i + 1 : n - 1]);
+    l0[i] = (j & 1) ? hi : lo;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) l1[i] = (j & 2) ? opq(l0[2 * i + 1]) : opq(l0[2 * i]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) l2[i] = (j & 4) ? opq(l1[2 * i + 1]) : opq(l1[2 * i]);
+  return (j & 8) ? opq(l2[1]) : opq(l2[0]);
+}
+
+template <class T>
+__device__ __forceinline__ void chol4(const T H[16], T L[10]) {
+  // L packed lower: L00 L10 L11 L20 L21 L22 L30 L31 L32 L33 (diagonal holds 1/L_ii)
+  T l00 = sqrt(H[0]);
+  T i00 = T(1) / l00;
+  T l10 = H[4] * i00, l20 = H[8] * i00, l30 = H[12] * i00;
+  T l11 = sqrt(H[5] - l10 * l10);
+  T i11 = T(1) / l11;
+  T l21 = (H[9] - l20 * l10) * i11, l31 = (H[13] - l30 * l10) * i11;
+  T l22 = sqrt(H[10] - l20 * l20 - l21 * l21);
+  T i22 = T(1) / l22;
+  T l32 = (H[14] - l30 * l20 - l31 * l21) * i22;
+  T l33 = sqrt(H[15] - l30 * l30 - l31 * l31 - l32 * l32);
+  T i33 = T(1) / l33;
+  L[0] = i00; L[1] = l10; L[2] = i11; L[3] = l20; L[4] = l21; L[5] = i22;
+  L[6] = l30; L[7] = l31; L[8] = l32; L[9] = i33;
+}
+
+template <class T>
+__device__ __forceinline__ void chol4_solve(const T L[10], const T b[4], T x[4]) {
+  // forward L y = b, backward L^T x = y
+  T y0 = b[0] * L[0];
+  T y1 = (b[1] - L[1] * y0) * L[2];
+  T y2 = (b[2] - L[3] * y0 - L[4] * y1) * L[5];
+  T y3 = (b[3] - L[6] * y0 - L[7] * y1 - L[8] * y2) * L[9];
+  x[3] = y3 * L[9];
+  x[2] = (y2 - L[8] * x[3]) * L[5];
+  x[1] = (y1 - L[4] * x[2] - L[7] * x[3]) * L[2];
+  x[0] = (y0 - L[1] * x[1] - L[3] * x[2] - L[6] * x[3]) * L[0];
+}
+
+template <int n, class T>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, T* out) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) out[i] = p[i];
+}
+
+template <class T, int BOX>
+__global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
+  __shared__ GroupLds<T> lds_all[GROUPS];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4;
+  const int j = lane & 15;
+  const int jx = j < NX ? j : 0;       // clamped state index
+  const int ju = j >= NX ? j - NX : 0; // clamped input index
+  GroupLds<T>& L = lds_all[q];
+  const int N = a.N;
+  constexpr int RN = Rec<BOX>::n;
+  const T s = a.s;
+  const Weights<T>& W = *a.W;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  T* slot = a.scratch + (int64_t)blockIdx.x * a.slot_elems;
+  T* XU = slot;                                        // [(N+1)][64]       xbar | ubar
+  T* KR = slot + (int64_t)(N + 1) * 64;                // [N][64][RN]       gains (+box extras)
+
+  for (int64_t wave = blockIdx.x; wave * GROUPS < a.B; wave += gridDim.x) {
+    const int64_t b_raw = wave * GROUPS + q;
+    const bool valid = b_raw < a.B;
+    const int64_t b = valid ? b_raw : a.B - 1;   // inactive groups recompute the last instance
+    T w[3] = {T(0), T(0), T(0)};
+    if (a.wind) {
+      w[0] = a.wind[b * a.wind_sb + 0];
+      w[1] = a.wind[b * a.wind_sb + 1];
+      w[2] = a.wind[b * a.wind_sb + 2];
+    }
+    const T* xr = a.xref + b * a.xref_sb;
+    const T* ur = a.uref + b * a.uref_sb;
+    const T* x0p = a.x0 + b * a.x0_sb;
+
+    // ------------------------------------------------------------------ pass 1: iterate
+    if (!iterate) {
+      T xb[NX], ub[NU];
+      load_vec<NX>(x0p, xb);
+      for (int k = 0; k < N; ++k) {
+        load_vec<NU>(ur + (int64_t)k * NU, ub);
+        XU[(int64_t)k * 64 + lane] = (j < NX) ? sel<NX>(xb, j) : sel<NU>(ub, ju);
+        T xn[NX], dd[1];
+        rk4<T, false>(xb, nullptr, ub, nullptr, a.h, a.M, w, xn, dd);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xb[i] = xn[i];
+      }
+      XU[(int64_t)N * 64 + lane] = (j < NX) ? sel<NX>(xb, j) : T(0);
+    } else {
+      const T* xbp = a.xbar + b * (int64_t)(N + 1) * NX;
+      const T* ubp = a.ubar + b * (int64_t)N * NU;
+      for (int k = 0; k <= N; ++k) {
+        const T vx = xbp[(int64_t)k * NX + jx];
+        const T vu = (k < N) ? ubp[(int64_t)k * NU + ju] : T(0);
+        XU[(int64_t)k * 64 + lane] = (j < NX) ? vx : vu;
+      }
+    }
+    __syncthreads();
+
+    uint64_t low[NU], up[NU];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) { low[m] = 0; up[m] = 0; }
+    bool done = false;
+    int32_t st = MPCB_STATUS_OK;
+
+    for (int it = 0;; ++it) {
+      // ------------------------------------------------------------------ pass 2: Riccati
+      T pj;       // p_{k+1}[j]
+      {
+        const T xN = XU[(int64_t)N * 64 + q * 16 + jx];
+        L.v[j] = (j < NX) ? xN - xr[(int64_t)N * NX + jx] : T(0);
+        __syncthreads();
+        T acc = T(0);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) acc += W.QN[jx * NX + i] * L.v[i];
+        pj = acc;
+        if (j < NX) {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) L.P[j * NX + i] = W.QN[i * NX + j];
+        }
+        __syncthreads();
+      }
+      T kff_out[NU];
+      bool qp_ok = true;
+      for (int k = N - 1; k >= 0; --k) {
+        T col[NX];
+        {
+          T xb[NX], ub[NU];
+          const T* p = XU + (int64_t)k * 64 + q * 16;
+          load_vec<NX>(p, xb);
+          load_vec<NU>(p + NX, ub);
+          // e = ybar - yref (component j), exchanged through LDS for block-diagonal W
+          const T ybar = XU[(int64_t)k * 64 + lane];
+          L.v[j] = ybar - ((j < NX) ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
+          // tangent RK4: column j of [A|B]
+          T dx[NX], du[NU], phi[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
+#pragma unroll
+          for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
+          rk4<T, true>(xb, dx, ub, du, a.h, a.M, w, phi, col);
+          // gap b = Phi(xbar_k, ubar_k) - xbar_{k+1};  pt = p + P b  (P symmetric: row j = col j)
+          T pt = pj;
+          if (iterate) {
+            const T* pn = XU + (int64_t)(k + 1) * 64 + q * 16;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pt += L.P[jx * NX + i] * (phi[i] - pn[i]);
+          }
+          L.hv[j] = pt;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
+        __syncthreads();
+        // h_j = col_j . pt
+        T hj = T(0);
+#pragma unroll
+        for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
+        // y = P col_j
+        T y[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) y[i] = T(0);
+#pragma unroll
+        for (int l = 0; l < NX; ++l) {
+          const T cl = col[l];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) y[i] += L.P[l * NX + i] * cl;
+        }
+        // G[:, j] = [A|B]^T y  + s * blkdiag(Q, R)[:, j]
+        T G[NZ];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) {
+          T acc = T(0);
+#pragma unroll
+          for (int l = 0; l < NX; ++l) acc += L.X[i * NX + l] * y[l];
+          G[i] = acc;
+        }
+        {
+          T acc = T(0);
+          if (j < NX) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+              G[i] += s * W.Q[i * NX + jx];
+              acc += W.Q[jx * NX + i] * L.v[i];
+            }
+          } else {
+#pragma unroll
+            for (int n = 0; n < NU; ++n) {
+              G[NX + n] += s * W.R[n * NU + ju];
+              acc += W.R[ju * NU + n] * L.v[NX + n];
+            }
+          }
+          hj += s * acc;
+        }
+#pragma unroll
+        for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
+        __syncthreads();   // all reads of L.v / L.hv / L.X done; Hu visible
+        L.hv[j] = hj;
+        __syncthreads();
+        T Ht[NU * NU], ht[NU], Hux_t[NU];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
+#pragma unroll
+          for (int n = 0; n < NU; ++n) Ht[m * NU + n] = L.Hu[(NX + n) * NU + m];
+          ht[m] = L.hv[NX + m];
+          Hux_t[m] = G[NX + m];
+        }
+        // ---- input-box masking (fixed components: du_m = delta_m)
+        if constexpr (BOX) {
+          T ub[NU];
+          load_vec<NU>(XU + (int64_t)k * 64 + q * 16 + NX, ub);
+          bool fixed[NU];
+          T delta[NU];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            const bool lo = (low[m] >> k) & 1ull, hi = (up[m] >> k) & 1ull;
+            fixed[m] = lo || hi;
+            delta[m] = lo ? (W.lbu[m] - ub[m]) : (hi ? (W.ubu[m] - ub[m]) : T(0));
+          }
+          T hn[NU];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            T acc = ht[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) acc += fixed[n] ? Ht[m * NU + n] * delta[n] : T(0);
+            hn[m] = fixed[m] ? -delta[m] : acc;
+            Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
+          }
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            ht[m] = hn[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) {
+              const bool f = fixed[m] || fixed[n];
+              Ht[m * NU + n] = f ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+            }
+          }
+        }
+        T Lc[10];
+        chol4(Ht, Lc);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) ok = ok && (Lc[i] == Lc[i]);
+        qp_ok = qp_ok && ok;
+        T kff[NU], Kj[NU], nh[NU];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -ht[m];
+        chol4_solve(Lc, nh, kff);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -Hux_t[m];
+        chol4_solve(Lc, nh, Kj);
+        // p_new = h_x + H_ux^T kff (unmasked H_ux);  P_new col j = G[0:12] + H_ux^T K[:, j]
+        T pn = hj;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
+        T Pn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          T acc = G[i];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
+          Pn[i] = acc;
+        }
+        // ---- store gains (and box extras)
+        T* rec = KR + ((int64_t)k * 64 + lane) * RN;
+        if (j < NX) {
+#pragma unroll
+          for (int m = 0; m < NU; ++m) rec[m] = Kj[m];
+        } else {
+          rec[0] = sel<NU>(kff, ju);
+          if constexpr (BOX) {
+            // row NX+m of the stage Hessian (== this lane's column by symmetry) and h_u[m]
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) rec[4 + i] = G[i];
+            rec[4 + NZ] = hj;
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < NU; ++m) kff_out[m] = kff[m];
+        __syncthreads();   // everyone finished reading L.P / L.Hu
+        if (j < NX) {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) L.P[j * NX + i] = Pn[i];
+        }
+        pj = pn;
+        __syncthreads();
+      }
+      if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
+
+      // ------------------------------------------------------------------ pass 3: forward
+      const bool need_fwd = BOX || a.X != nullptr || a.U != nullptr || iterate;
+      uint64_t nlow = 0, nup = 0;   // lanes NX+m: new active sets of component m
+      T u0v[NU];
+      if (need_fwd) {
+        T dxk[NX];
+        {
+          const T* p = XU + q * 16;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) dxk[i] = iterate ? x0p[i] - p[i] : T(0);
+        }
+        const bool write = valid && !done;
+        for (int k = 0; k < N; ++k) {
+          T duk[NU];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) duk[m] = KR[((int64_t)k * 64 + q * 16 + NX + m) * RN];
+#pragma unroll
+          for (int l = 0; l < NX; ++l) {
+            const T* r = KR + ((int64_t)k * 64 + q * 16 + l) * RN;
+#pragma unroll
+            for (int m = 0; m < NU; ++m) duk[m] += r[m] * dxk[l];
+          }
+          T xb[NX], ub[NU];
+          const T* p = XU + (int64_t)k * 64 + q * 16;
+          load_vec<NX>(p, xb);
+          load_vec<NU>(p + NX, ub);
+          if (k == 0) {
+#pragma unroll
+            for (int m = 0; m < NU; ++m) u0v[m] = ub[m] + duk[m];
+          }
+          if constexpr (BOX) {
+            if (j >= NX) {
+              const int m = ju;
+              const T* r = KR + ((int64_t)k * 64 + lane) * RN;
+              const bool lo = (sel<NU>(low, m) >> k) & 1ull, hi = (sel<NU>(up, m) >> k) & 1ull;
+              T mu = r[4 + NZ];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) mu += r[4 + i] * dxk[i];
+#pragma unroll
+              for (int n = 0; n < NU; ++n) mu += r[4 + NX + n] * duk[n];
+              mu = (lo || hi) ? mu : T(0);
+              const T uk = sel<NU>(ub, m) + sel<NU>(duk, m);
+              const T lb = W.lbu[m], ubd = W.ubu[m];
+              const bool nl = mu + (lb - uk) > T(0);
+              const bool nu_ = mu + (ubd - uk) < T(0);
+              nlow |= (uint64_t)nl << k;
+              nup |= (uint64_t)nu_ << k;
+            }
+          }
+          if (write) {
+            if (a.X && j < NX) a.X[(b * (N + 1) + k) * NX + j] = sel<NX>(xb, j) + sel<NX>(dxk, j);
+            if (a.U && j >= NX) a.U[(b * N + k) * NU + ju] = sel<NU>(ub, ju) + sel<NU>(duk, ju);
+          }
+          T phi[NX], dphi[NX];
+          rk4<T, true>(xb, dxk, ub, duk, a.h, a.M, w, phi, dphi);
+          if (iterate) {
+            const T* pn = XU + (int64_t)(k + 1) * 64 + q * 16;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dxk[i] = dphi[i] + (phi[i] - pn[i]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dxk[i] = dphi[i];
+          }
+        }
+        if (write && a.X && j < NX) {
+          const T xN = XU[(int64_t)N * 64 + q * 16 + jx];
+          a.X[(b * (N + 1) + N) * NX + j] = xN + sel<NX>(dxk, j);
+        }
+      } else {
+        T ub[NU];
+        load_vec<NU>(XU + q * 16 + NX, ub);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) u0v[m] = ub[m] + kff_out[m];
+      }
+      if (valid && !done && j >= NX) a.u0[b * NU + ju] = sel<NU>(u0v, ju);
+
+      if constexpr (!BOX) {
+        break;
+      } else {
+        // active-set update: converged when every component's sets repeat
+        bool changed = false;
+        if (j >= NX) changed = (nlow != sel<NU>(low, ju)) || (nup != sel<NU>(up, ju));
+        const uint64_t ball = __ballot(changed);
+        const bool gchanged = ((ball >> (q * 16)) & 0xFFFFull) != 0;
+        // broadcast the new sets from lanes NX..NX+3 of the group
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
+          const int src = q * 16 + NX + m;
+          const uint64_t nl = __shfl(nlow, src);
+          const uint64_t nu_ = __shfl(nup, src);
+          if (!done) { low[m] = nl; up[m] = nu_; }
+        }
+        if (!done && !gchanged) done = true;
+        const bool all_done = __all(done || !valid);
+        if (all_done) break;
+        if (it + 1 >= a.max_as_iter) {
+          if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // status: acados-style codes; NaN guard on u0
+    if (valid && j == NX) {
+      T u0c[NU];
+      load_vec<NU>(a.u0 + b * NU, u0c);
+      bool fin = true;
+#pragma unroll
+      for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+      a.status[b] = fin ? st : MPCB_STATUS_NAN;
+    }
+    __syncthreads();
+  }
+}
+
+template <class T> int64_t solve_slot_elems(int N, int box) {
+  const int RN = box ? Rec<1>::n : Rec<0>::n;
+  return (int64_t)(N + 1) * 64 + (int64_t)N * 64 * RN;
+}
+
+template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipStream_t st) {
+  if (a.box)
+    hipLaunchKernelGGL((solve_kernel<T, 1>), dim3(grid), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL((solve_kernel<T, 0>), dim3(grid), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+template hipError_t launch_solve<double>(const SolveArgs<double>&, int, hipStream_t);
+template hipError_t launch_solve<float>(const SolveArgs<float>&, int, hipStream_t);
+template int64_t solve_slot_elems<double>(int, int);
+template int64_t solve_slot_elems<float>(int, int);
+
+}  // namespace mpcb

@@ -1,0 +1,298 @@
+"""One Gauss-Newton SQP_RTI step of the BLASTER LINEAR_LS OCP (oracle; test infrastructure only).
+
+Problem (``blastermodel.py:226-287``; numbers pinned by ``acados_ocp_blasterModel.json``):
+
+    min  sum_{k<N} s_k/2 (|x_k - xr_k|_Q^2 + |u_k - ur_k|_R^2) + 1/2 |x_N - xr_N|_QN^2
+    s.t. x_0 = x0                               (lbx_0 = ubx_0 = x, simulation_blaster.py:60-61)
+         x_{k+1} = Phi(x_k, u_k)                 (RK4, oracle.rk4)
+         lbu <= u_k <= ubu                       (idxbu, blastermodel.py:261-264; optional)
+
+W = blkdiag(Q, R), W_e = QN (``blastermodel.py:244-245``); V are selectors (``:247-254``) so
+the Gauss-Newton Hessian is blkdiag(Q, R).  s_k = cost_scale (default dt = Tf/N) for k < N,
+1 at the terminal stage: the acados template sets the LS cost "scaling" to ``time_steps[k]``
+[acados 0.1.x convention, third-party, unpinned — switchable via ``cost_scale``].
+
+SQP_RTI (``nlp_solver_type='SQP_RTI'``, JSON ``globalization=FIXED_STEP``,
+``nlp_solver_step_length=1.0``): linearise at the iterate (xbar, ubar), solve the LQ QP in
+(dx, du) with gaps b_k = Phi(xbar_k, ubar_k) - xbar_{k+1}, take the full step.  ``X`` is the
+linear prediction xbar + dx (what ``ocp_solver.get(k, 'x')`` returns), ``U = ubar + du``.
+
+Two linearisation modes:
+
+* ``rollout`` (the batch ``solve(x0, x_ref, u_ref)`` surface): ubar = u_ref, xbar = RK4 rollout
+  from x0 (gap-free, dx_0 = 0).
+* ``iterate`` (the acados facade): xbar, ubar supplied (the persistent SQP_RTI iterate).
+
+QP solvers here:
+
+* ``riccati_solve``: Riccati recursion (HPIPM's OCP-QP structure; the QP is strictly convex so
+  its minimiser is unique and method-independent).  Input boxes are handled by an exact
+  primal-dual active-set (PDAS) loop around a masked Riccati — the same algorithm the device
+  runs.  HPIPM instead uses an interior-point method; both converge to the same unique
+  minimiser, to within HPIPM's tolerance.  [parity unpinned: HPIPM absent]
+* ``dense_box_qp`` (tests only): condensed QP solved by SciPy BVLS, an independent exact check.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .model import Params, f12
+from .rk4 import rk4_sens, rk4_step
+
+NX, NU = 12, 4
+STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
+
+
+def default_Q() -> np.ndarray:
+    # simulation_blaster.py:24 sliced to the 12 rigid-body states (JSON cost.W diag[0:12])
+    return np.diag([1e3] * 6 + [5.0] * 3 + [10.0] * 3)
+
+
+def default_R() -> np.ndarray:
+    # simulation_blaster.py:27 sliced to the 4 motor thrusts (JSON cost.W diag[17:21])
+    return np.diag([0.05] * 4)
+
+
+@dataclass
+class OcpSpec:
+    N: int = 20
+    dt: float = 1.0 / 30.0
+    Q: np.ndarray = field(default_factory=default_Q)
+    R: np.ndarray = field(default_factory=default_R)
+    QN: np.ndarray | None = None            # default 10 * Q (simulation_blaster.py:25)
+    cost_scale: float | None = None         # default dt (acados time_steps scaling)
+    lbu: np.ndarray | None = None           # None -> unconstrained
+    ubu: np.ndarray | None = None
+    params: Params = field(default_factory=Params)
+    max_as_iter: int = 50
+
+    def __post_init__(self):
+        if self.QN is None:
+            self.QN = 10.0 * np.asarray(self.Q)
+
+    @property
+    def s(self) -> float:
+        return self.dt if self.cost_scale is None else self.cost_scale
+
+    @property
+    def boxed(self) -> bool:
+        return self.lbu is not None
+
+
+def rollout(x0, ubar, spec: OcpSpec, wind=None):
+    B = x0.shape[0]
+    X = np.empty((B, spec.N + 1, NX))
+    X[:, 0] = x0
+    for k in range(spec.N):
+        X[:, k + 1] = rk4_step(X[:, k], ubar[:, k], spec.dt, spec.params, wind)
+    return X
+
+
+def linearise(xbar, ubar, spec: OcpSpec, wind=None):
+    """A_k, B_k, gaps b_k at the iterate."""
+    B = xbar.shape[0]
+    N = spec.N
+    A = np.empty((B, N, NX, NX))
+    Bm = np.empty((B, N, NX, NU))
+    gap = np.empty((B, N, NX))
+    for k in range(N):
+        xn, A[:, k], Bm[:, k] = rk4_sens(xbar[:, k], ubar[:, k], spec.dt, spec.params, wind)
+        gap[:, k] = xn - xbar[:, k + 1]
+    return A, Bm, gap
+
+
+def _masked_stage(Huu, Hux, hu, fixed, delta):
+    """Eliminate fixed input components (value du_m = delta_m) from the stage QP."""
+    Ht = Huu.copy()
+    Hxt = Hux.copy()
+    ht = hu.copy()
+    if fixed is not None and fixed.any():
+        # free rows: h_F += H_FA delta_A
+        ht = ht + np.einsum('bij,bj->bi', Huu, np.where(fixed, delta, 0.0))
+        eye = np.eye(NU)[None]
+        fr = fixed[:, :, None] | fixed[:, None, :]
+        diag = fixed[:, :, None] & fixed[:, None, :] & (eye > 0)
+        Ht = np.where(fr, 0.0, Ht)
+        Ht = np.where(diag, 1.0, Ht)
+        Hxt = np.where(fixed[:, :, None], 0.0, Hxt)
+        ht = np.where(fixed, -delta, ht)
+    return Ht, Hxt, ht
+
+
+def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
+                  fixed=None, delta=None):
+    """Solve the (masked) LQ QP.  Returns dx (B,N+1,NX), du (B,N,NU), mu (B,N,NU), ok (B,)."""
+    Bsz, N = xbar.shape[0], spec.N
+    s = spec.s
+    Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
+    P = np.broadcast_to(QN, (Bsz, NX, NX)).copy()
+    p = np.einsum('ij,bj->bi', QN, xbar[:, N] - xref[:, N])
+    K = np.empty((Bsz, N, NU, NX))
+    kff = np.empty((Bsz, N, NU))
+    Huus = np.empty((Bsz, N, NU, NU))
+    Huxs = np.empty((Bsz, N, NU, NX))
+    hus = np.empty((Bsz, N, NU))
+    ok = np.ones(Bsz, dtype=bool)
+    for k in range(N - 1, -1, -1):
+        Ak, Bk, bk = A[:, k], Bm[:, k], gap[:, k]
+        pt = p + np.einsum('bij,bj->bi', P, bk)
+        PA = np.einsum('bij,bjk->bik', P, Ak)
+        PB = np.einsum('bij,bjk->bik', P, Bk)
+        Hxx = s * Q + np.einsum('bji,bjk->bik', Ak, PA)
+        Hux = np.einsum('bji,bjk->bik', Bk, PA)
+        Huu = s * R + np.einsum('bji,bjk->bik', Bk, PB)
+        hx = s * np.einsum('ij,bj->bi', Q, xbar[:, k] - xref[:, k]) + np.einsum('bji,bj->bi', Ak, pt)
+        hu = s * np.einsum('ij,bj->bi', R, ubar[:, k] - uref[:, k]) + np.einsum('bji,bj->bi', Bk, pt)
+        fk = None if fixed is None else fixed[:, k]
+        dk = None if delta is None else delta[:, k]
+        Ht, Hxt, ht = _masked_stage(Huu, Hux, hu, fk, dk)
+        try:
+            L = np.linalg.cholesky(Ht)
+        except np.linalg.LinAlgError:
+            ev_ok = np.all(np.linalg.eigvalsh(Ht) > 0, axis=-1)
+            ok &= ev_ok
+            Ht = np.where(ev_ok[:, None, None], Ht, np.eye(NU)[None])
+            L = np.linalg.cholesky(Ht)
+        Kk = -np.linalg.solve(Ht, Hxt)
+        kk = -np.linalg.solve(Ht, ht[..., None])[..., 0]
+        K[:, k], kff[:, k] = Kk, kk
+        Huus[:, k], Huxs[:, k], hus[:, k] = Huu, Hux, hu
+        P = Hxx + np.einsum('bji,bjk->bik', Hux, Kk)
+        P = 0.5 * (P + np.swapaxes(P, 1, 2))
+        p = hx + np.einsum('bji,bj->bi', Hux, kk)
+        del L
+    dx = np.empty((Bsz, N + 1, NX))
+    du = np.empty((Bsz, N, NU))
+    mu = np.empty((Bsz, N, NU))
+    dx[:, 0] = dx0
+    for k in range(N):
+        du[:, k] = np.einsum('bij,bj->bi', K[:, k], dx[:, k]) + kff[:, k]
+        mu[:, k] = (np.einsum('bij,bj->bi', Huus[:, k], du[:, k])
+                    + np.einsum('bij,bj->bi', Huxs[:, k], dx[:, k]) + hus[:, k])
+        dx[:, k + 1] = (np.einsum('bij,bj->bi', A[:, k], dx[:, k])
+                        + np.einsum('bij,bj->bi', Bm[:, k], du[:, k]) + gap[:, k])
+    return dx, du, mu, ok
+
+
+def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
+    """Primal-dual active set on input boxes around the masked Riccati.
+
+    Returns dx, du, status, iterations.  Active sets: low = {mu + c(lb-u) > 0},
+    up = {mu + c(ub-u) < 0} with c = 1 (Hintermueller-Ito-Kunisch); converged when the sets
+    repeat, at which point the KKT conditions hold exactly.
+    """
+    Bsz, N = xbar.shape[0], spec.N
+    lb = np.broadcast_to(np.asarray(spec.lbu, dtype=np.float64), (NU,))
+    ub = np.broadcast_to(np.asarray(spec.ubu, dtype=np.float64), (NU,))
+    dx, du, mu, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+    u = ubar + du
+    low = u < lb
+    up = u > ub
+    done = np.zeros(Bsz, dtype=bool)
+    iters = np.zeros(Bsz, dtype=np.int32)
+    out_dx, out_du = dx.copy(), du.copy()
+    for it in range(spec.max_as_iter):
+        fixed = low | up
+        delta = np.where(low, lb - ubar, np.where(up, ub - ubar, 0.0))
+        dx, du, mu, ok2 = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, fixed, delta)
+        ok &= ok2
+        u = ubar + du
+        mu = np.where(fixed, mu, 0.0)
+        nlow = mu + (lb - u) > 0
+        nup = mu + (ub - u) < 0
+        conv = np.all((nlow == low) & (nup == up), axis=(1, 2))
+        newly = conv & ~done
+        out_dx[newly], out_du[newly] = dx[newly], du[newly]
+        iters[~done] += 1
+        done |= conv
+        low = np.where(done[:, None, None], low, nlow)
+        up = np.where(done[:, None, None], up, nup)
+        if done.all():
+            break
+    out_dx[~done], out_du[~done] = dx[~done], du[~done]
+    status = np.where(done, STATUS_OK, STATUS_MAXITER).astype(np.int32)
+    status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
+    return out_dx, out_du, status, iters
+
+
+def mpc_solve(x0, xref, uref, spec: OcpSpec, wind=None, mode='rollout', xbar=None, ubar=None,
+              return_lin=False):
+    """One SQP_RTI step for a batch.  x0 (B,12), xref (B,N+1,12), uref (B,N,4)."""
+    x0 = np.asarray(x0, dtype=np.float64)
+    Bsz, N = x0.shape[0], spec.N
+    xref = np.broadcast_to(np.asarray(xref, dtype=np.float64), (Bsz, N + 1, NX))
+    uref = np.broadcast_to(np.asarray(uref, dtype=np.float64), (Bsz, N, NU))
+    if mode == 'rollout':
+        ubar = uref.copy()
+        xbar = rollout(x0, ubar, spec, wind)
+    else:
+        xbar = np.asarray(xbar, dtype=np.float64)
+        ubar = np.asarray(ubar, dtype=np.float64)
+    A, Bm, gap = linearise(xbar, ubar, spec, wind)
+    dx0 = x0 - xbar[:, 0]
+    if spec.boxed:
+        dx, du, status, iters = pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+    else:
+        dx, du, _, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+        status = np.where(ok, STATUS_OK, STATUS_QP_FAIL).astype(np.int32)
+        iters = np.zeros(Bsz, dtype=np.int32)
+    X = xbar + dx
+    U = ubar + du
+    bad = ~(np.isfinite(X).all(axis=(1, 2)) & np.isfinite(U).all(axis=(1, 2)))
+    status = np.where(bad, STATUS_NAN, status).astype(np.int32)
+    out = dict(u0=U[:, 0].copy(), X=X, U=U, status=status, iters=iters, xbar=xbar, ubar=ubar)
+    if return_lin:
+        out.update(A=A, B=Bm, gap=gap)
+    return out
+
+
+def stage_cost(X, U, xref, uref, spec: OcpSpec) -> np.ndarray:
+    """Objective at (X, U) — what acados ``get_cost()`` reports for the new iterate."""
+    s = spec.s
+    Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
+    ex = X[:, :-1] - xref[:, :-1]
+    eu = U - uref
+    eN = X[:, -1] - xref[:, -1]
+    c = 0.5 * s * (np.einsum('bki,ij,bkj->b', ex, Q, ex) + np.einsum('bki,ij,bkj->b', eu, R, eu))
+    return c + 0.5 * np.einsum('bi,ij,bj->b', eN, QN, eN)
+
+
+def dense_box_qp(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
+    """Independent check (tests only): condense the QP in du and solve it with SciPy BVLS."""
+    from scipy.optimize import lsq_linear
+
+    Bsz, N = xbar.shape[0], spec.N
+    s = spec.s
+    Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
+    out_du = np.empty((Bsz, N, NU))
+    for b in range(Bsz):
+        # dx_k = c_k + G_k du  (G_k: NX x N*NU)
+        c = np.zeros((N + 1, NX))
+        G = np.zeros((N + 1, NX, N * NU))
+        c[0] = dx0[b]
+        for k in range(N):
+            c[k + 1] = A[b, k] @ c[k] + gap[b, k]
+            G[k + 1] = A[b, k] @ G[k]
+            G[k + 1][:, k * NU:(k + 1) * NU] += Bm[b, k]
+        H = np.zeros((N * NU, N * NU))
+        g = np.zeros(N * NU)
+        for k in range(N + 1):
+            W = QN if k == N else s * Q
+            e = c[k] + xbar[b, k] - xref[b, k]
+            H += G[k].T @ W @ G[k]
+            g += G[k].T @ W @ e
+        for k in range(N):
+            sl = slice(k * NU, (k + 1) * NU)
+            H[sl, sl] += s * R
+            g[sl] += s * R @ (ubar[b, k] - uref[b, k])
+        L = np.linalg.cholesky(H)            # H = L L^T ; min 1/2|L^T z + L^{-1} g|^2
+        Lt = L.T
+        rhs = -np.linalg.solve(L, g)
+        lb = np.tile(np.asarray(spec.lbu, dtype=np.float64), N) - ubar[b].reshape(-1)
+        ub = np.tile(np.asarray(spec.ubu, dtype=np.float64), N) - ubar[b].reshape(-1)
+        res = lsq_linear(Lt, rhs, bounds=(lb, ub), method='bvls', tol=1e-14, lsmr_tol='auto',
+                         max_iter=10000)
+        out_du[b] = res.x.reshape(N, NU)
+    return out_du

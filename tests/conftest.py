@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def pytest_collection_modifyitems(config, items):
+    # GPU tests are selected with -m gpu; on a machine without a GPU they are skipped loudly
+    try:
+        import torch
+        have_gpu = torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        have_gpu = False
+    if have_gpu:
+        return
+    skip = pytest.mark.skip(reason="no GPU visible (torch.cuda.is_available() is False)")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)

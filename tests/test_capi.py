@@ -1,0 +1,81 @@
+"""CPU-side checks of the drop-in boundary: the HIP library builds, loads and exports every
+symbol include/mpcb.h declares; the ctypes struct mirrors ``mpcb_config``; the host-side
+config validation mirrors the reference constructor's arguments."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, 'include', 'mpcb.h')
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r'\b(mpcb_[a-z_]+)\s*\(', txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mpc_blaster_amd import _lib
+    from mpc_blaster_amd.build import build
+    build()
+    lib = _lib.load()
+    declared = _declared()
+    assert len(declared) >= 11
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(_lib.EXPORTS) == set(declared)
+    assert lib.mpcb_abi_version() == 1
+
+
+def test_config_struct_layout_matches_header():
+    from mpc_blaster_amd import _lib
+    # 8 int32 (32 B) + 8 doubles + J[9] + Q[289] + R[36] + QN[289] + lbu[6] + ubu[6]
+    n_doubles = 8 + 9 + 289 + 36 + 289 + 6 + 6
+    assert ctypes.sizeof(_lib.MpcbConfig) == 32 + 8 * n_doubles
+    # compile a tiny C program against the header and compare sizeof/offsetof
+    import subprocess
+    import tempfile
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "mpcb.h"
+int main(void) { printf("%zu %zu %zu %zu\n", sizeof(mpcb_config), offsetof(mpcb_config, dt),
+  offsetof(mpcb_config, Q), offsetof(mpcb_config, lbu)); return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, 'm.c')
+        open(c, 'w').write(src)
+        exe = os.path.join(d, 'm')
+        subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), c, '-o', exe])
+        out = subprocess.check_output([exe]).decode().split()
+    C = _lib.MpcbConfig
+    assert [int(v) for v in out] == [ctypes.sizeof(C), C.dt.offset, C.Q.offset, C.lbu.offset]
+
+
+def test_create_without_gpu_fails_cleanly():
+    """On a GPU-less host mpcb_create reports an error instead of crashing."""
+    torch = pytest.importorskip('torch')
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from mpc_blaster_amd import MPCConfig, _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    c = MPCConfig().to_c()
+    rc = lib.mpcb_create(ctypes.byref(c), 0, 16, ctypes.byref(h))
+    assert rc != 0 and not h.value
+    assert lib.mpcb_last_error()
+
+
+def test_config_validation():
+    from mpc_blaster_amd import MPCConfig
+    with pytest.raises(ValueError):
+        MPCConfig(Q=np.eye(17))
+    with pytest.raises(ValueError):
+        MPCConfig(lbu=np.zeros(4))
+    c = MPCConfig(N=30, lbu=np.zeros(4), ubu=np.full(4, 65.0))
+    cc = c.to_c()
+    assert cc.box_u == 1 and cc.N == 30 and abs(cc.cost_scale - 1 / 30) < 1e-15
+    assert list(cc.ubu)[:4] == [65.0] * 4

@@ -1,0 +1,184 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle on identical inputs.
+
+Tolerances (north_star: 1e-5 relative in fp64):
+* fp64: per-instance ||y_dev - y_oracle||_inf / max(||y_oracle||_inf, 1) <= 1e-9 (achieved
+  ~1e-12; RK4/trig rounding only).
+* fp32: the same normwise metric <= 2e-4 on X and <= 5e-4 on u0 (fp32 Riccati, SURVEY §7 ii);
+  the achieved numbers are printed by tests and recorded in DESIGN.md.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.inputs import make_inputs
+from oracle.model import Params
+from oracle.ocp import OcpSpec, mpc_solve
+from oracle.rk4 import rk4_sens
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def _mpc(N, dtype='f64', box=False, max_batch=4096, **kw):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    cfg = MPCConfig(N=N, dtype=dtype, lbu=np.zeros(4) if box else None,
+                    ubu=np.full(4, 65.0) if box else None, **kw)
+    return BatchedMPC(cfg, max_batch=max_batch)
+
+
+def _spec(N, box=False):
+    return OcpSpec(N=N, lbu=np.zeros(4) if box else None, ubu=np.full(4, 65.0) if box else None)
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, dtype=np.float64).reshape(b.shape[0], -1)
+    return np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1.0)
+
+
+def test_library_is_the_native_hip_build():
+    from mpc_blaster_amd import _lib
+    lib = _lib.load()
+    assert os.path.basename(lib._name) == 'libmpcblaster.so'
+    assert lib.mpcb_abi_version() == 1
+
+
+def test_linearize_matches_oracle_fp64():
+    N, B = 5, 37
+    m = _mpc(N, 'f64', max_batch=B)
+    rng = np.random.default_rng(5)
+    xb = rng.uniform(-0.6, 0.6, (B, N + 1, 12))
+    ub = rng.uniform(5.0, 40.0, (B, N, 4))
+    A, Bm, xn = (t.cpu().numpy() for t in m.linearize(xb, ub))
+    P = Params()
+    for k in range(N):
+        xr, Ar, Br = rk4_sens(xb[:, k], ub[:, k], 1.0 / 30.0, P)
+        assert np.abs(A[:, k] - Ar).max() < 1e-12
+        assert np.abs(Bm[:, k] - Br).max() < 1e-12
+        assert np.abs(xn[:, k] - xr).max() < 1e-12
+
+
+def test_gen_inputs_bit_exact_fp64():
+    m = _mpc(20, 'f64', max_batch=1000)
+    d = m.gen_inputs(1000, seed=1003, id_offset=123, ref='sine', wind=True)
+    o = make_inputs('c3', ids=np.arange(123, 1123, dtype=np.uint64))
+    assert np.array_equal(d['x0'].cpu().numpy(), o['x0'])
+    from oracle.inputs import make_wind, draws
+    assert np.array_equal(d['wind'].cpu().numpy(), make_wind(draws(1003, np.arange(123, 1123))))
+    assert np.abs(d['xref'].cpu().numpy() - o['xref']).max() < 1e-14
+    assert np.all(d['uref'].cpu().numpy() == 22.0725)
+
+
+def test_c1_golden_fp64():
+    d = np.load(os.path.join(GOLD, 'mpc_c1.npz'))
+    m = _mpc(10, 'f64', max_batch=1)
+    m.solve(d['x0'], d['xref'], d['uref'])
+    torch.cuda.synchronize()
+    assert relerr(m.get_control().cpu().numpy(), d['u0']).max() < 1e-9
+    assert relerr(m.get_state_trajectory().cpu().numpy(), d['X']).max() < 1e-9
+    assert relerr(m.get_input_trajectory().cpu().numpy(), d['U']).max() < 1e-9
+    assert m.get_status().cpu().numpy().tolist() == [0]
+
+
+@pytest.mark.parametrize('cfg,N,dtype,box', [
+    ('c2', 20, 'f64', False), ('c3', 20, 'f64', False), ('c3', 20, 'f32', False),
+    ('c4', 30, 'f64', True), ('c4', 30, 'f32', True), ('c2', 10, 'f32', False),
+])
+def test_solve_matches_oracle(cfg, N, dtype, box):
+    B = 203   # ragged: not a multiple of the 4-instance wave
+    inp = make_inputs(cfg, ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, dtype, box, max_batch=B)
+    m.solve(inp['x0'], inp['xref'], inp['uref'])
+    torch.cuda.synchronize()
+    u0 = m.get_control().cpu().numpy()
+    X = m.get_state_trajectory().cpu().numpy()
+    U = m.get_input_trajectory().cpu().numpy()
+    st = m.get_status().cpu().numpy()
+    # the oracle sees exactly the inputs the device saw (fp32 inputs rounded first)
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    o = mpc_solve(cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), _spec(N, box))
+    e_u, e_x, e_U = relerr(u0, o['u0']), relerr(X, o['X']), relerr(U, o['U'])
+    print(f'{cfg} N={N} {dtype} box={box}: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
+    assert (st == o['status']).all() and (st == 0).all()
+    tol_u, tol_x = (1e-9, 1e-9) if dtype == 'f64' else (5e-4, 2e-4)
+    assert e_u.max() < tol_u and e_U.max() < tol_u and e_x.max() < tol_x
+    if box:
+        assert (U >= -1e-6).all() and (U <= 65 + 1e-4).all()
+
+
+def test_iterate_mode_matches_oracle_fp64():
+    """acados SQP_RTI semantics: linearise at a given iterate with gaps and dx0 != 0."""
+    N, B = 12, 41
+    rng = np.random.default_rng(9)
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    xbar = inp['xref'] + rng.normal(scale=0.05, size=(B, N + 1, 12))
+    ubar = inp['uref'] + rng.normal(scale=1.0, size=(B, N, 4))
+    m = _mpc(N, 'f64', max_batch=B)
+    m.solve_iterate(inp['x0'], xbar, ubar, inp['xref'], inp['uref'])
+    torch.cuda.synchronize()
+    o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], _spec(N), mode='iterate', xbar=xbar, ubar=ubar)
+    assert relerr(m.get_control().cpu().numpy(), o['u0']).max() < 1e-9
+    assert relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max() < 1e-9
+
+
+def test_wind_extension_fp64():
+    N, B = 8, 16
+    inp = make_inputs('c5', ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, 'f64', max_batch=B)
+    m.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'])
+    torch.cuda.synchronize()
+    o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], _spec(N), wind=inp['wind'])
+    assert relerr(m.get_control().cpu().numpy(), o['u0']).max() < 1e-9
+
+
+def test_sim_step_and_histogram():
+    B = 1000
+    m = _mpc(20, 'f64', max_batch=B)
+    rng = np.random.default_rng(4)
+    x = rng.uniform(-0.5, 0.5, (B, 12))
+    u = rng.uniform(0, 65, (B, 4))
+    xo = m.sim_step(x, u).cpu().numpy()
+    from oracle.rk4 import rk4_step
+    assert np.abs(xo - rk4_step(x, u, 1.0 / 30.0, Params())).max() < 1e-12
+    counts = m.histogram(u, 0.0, 65.0, 64).cpu().numpy()
+    ref = np.stack([np.histogram(np.clip(u[:, i], 0, 65 - 1e-9), bins=64, range=(0, 65))[0] for i in range(4)])
+    assert np.array_equal(counts, ref)
+
+
+def test_u0_only_path_equals_full_path():
+    N, B = 20, 64
+    inp = make_inputs('c3', ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, 'f32', max_batch=B)
+    a = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=False).clone()
+    b = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_full_size_c3_properties():
+    """BASELINE c3 at full size: statuses, finiteness, shard invariance, sampled oracle parity."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    B, N = 65536, 20
+    m = BatchedMPC(MPCConfig(N=N, dtype='f32'), max_batch=B)
+    d = m.gen_inputs(B, seed=1003, ref='sine')
+    u0 = m.solve(d['x0'], d['xref'], d['uref'], want_traj=True).clone()
+    X = m.get_state_trajectory().clone()
+    st = m.get_status().clone()
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.isfinite(u0).all() and torch.isfinite(X).all()
+    # shard invariance: instances 40000.. solved alone give identical bits
+    sl = slice(40000, 40000 + 777)
+    u_sub = m.solve(d['x0'][sl], d['xref'][sl], d['uref'], want_traj=False)
+    torch.cuda.synchronize()
+    assert torch.equal(u_sub, u0[sl])
+    # sampled oracle parity
+    idx = np.arange(0, B, 4099)
+    x0 = d['x0'][idx].double().cpu().numpy()
+    xr = d['xref'][idx].double().cpu().numpy()
+    o = mpc_solve(x0, xr, np.full((len(idx), N, 4), np.float32(22.0725), dtype=np.float64), _spec(N))
+    assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-4
+    assert relerr(X[idx].cpu().numpy(), o['X']).max() < 2e-4
