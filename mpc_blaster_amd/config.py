@@ -45,7 +45,7 @@ class MPCConfig:
     cost_scale: float | None = None    # default dt
     lbu: np.ndarray | None = None      # None -> no input box
     ubu: np.ndarray | None = None
-    max_as_iter: int = 50
+    max_as_iter: int = 200
 
     def __post_init__(self):
         self.Q = np.asarray(self.Q, dtype=np.float64)

@@ -165,6 +165,7 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
     for (int m = 0; m < NU; ++m) { low[m] = 0; up[m] = 0; }
     bool done = false;
     int32_t st = MPCB_STATUS_OK;
+    int best = 0x7fffffff, pcount = 3;   // Kim-Park safeguard state (uniform per group)
 
     for (int it = 0;; ++it) {
       // ------------------------------------------------------------------ pass 2: Riccati
@@ -340,9 +341,15 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
 #pragma unroll
         for (int m = 0; m < NU; ++m) kff_out[m] = kff[m];
         __syncthreads();   // everyone finished reading L.P / L.Hu
+        // Store P_{k} symmetric by construction: entry (r, c) comes from lane max(r, c).  The
+        // plain column-wise update drifts antisymmetric and that drift is amplified stage to
+        // stage (fp32 u0 error 2e-1 -> 2e-6 with this, fp64 1e-7 -> 1e-15).
         if (j < NX) {
 #pragma unroll
-          for (int i = 0; i < NX; ++i) L.P[j * NX + i] = Pn[i];
+          for (int i = 0; i < NX; ++i) {
+            if (i <= j) L.P[j * NX + i] = Pn[i];
+            if (i < j) L.P[i * NX + j] = Pn[i];
+          }
         }
         pj = pn;
         __syncthreads();
@@ -351,7 +358,8 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
 
       // ------------------------------------------------------------------ pass 3: forward
       const bool need_fwd = BOX || a.X != nullptr || a.U != nullptr || iterate;
-      uint64_t nlow = 0, nup = 0;   // lanes NX+m: new active sets of component m
+      // lanes NX+m: infeasibility sets of component m (bit k = stage k)
+      uint64_t vlo = 0, vhi = 0, vfl = 0, vfu = 0;
       T u0v[NU];
       if (need_fwd) {
         T dxk[NX];
@@ -389,13 +397,12 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
               for (int i = 0; i < NX; ++i) mu += r[4 + i] * dxk[i];
 #pragma unroll
               for (int n = 0; n < NU; ++n) mu += r[4 + NX + n] * duk[n];
-              mu = (lo || hi) ? mu : T(0);
               const T uk = sel<NU>(ub, m) + sel<NU>(duk, m);
-              const T lb = W.lbu[m], ubd = W.ubu[m];
-              const bool nl = mu + (lb - uk) > T(0);
-              const bool nu_ = mu + (ubd - uk) < T(0);
-              nlow |= (uint64_t)nl << k;
-              nup |= (uint64_t)nu_ << k;
+              const bool fr = !(lo || hi);
+              vlo |= (uint64_t)(fr && uk < W.lbu[m]) << k;
+              vhi |= (uint64_t)(fr && uk > W.ubu[m]) << k;
+              vfl |= (uint64_t)(lo && mu < T(0)) << k;
+              vfu |= (uint64_t)(hi && mu > T(0)) << k;
             }
           }
           if (write) {
@@ -428,18 +435,32 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
       if constexpr (!BOX) {
         break;
       } else {
-        // active-set update: converged when every component's sets repeat
-        bool changed = false;
-        if (j >= NX) changed = (nlow != sel<NU>(low, ju)) || (nup != sel<NU>(up, ju));
-        const uint64_t ball = __ballot(changed);
-        const bool gchanged = ((ball >> (q * 16)) & 0xFFFFull) != 0;
-        // broadcast the new sets from lanes NX..NX+3 of the group
+        // active-set update (Kim-Park block principal pivoting, mirrors oracle.ocp.pdas_solve):
+        // V = {free u<lb} U {free u>ub} U {at lb, mu<0} U {at ub, mu>0}; |V| = 0 <=> KKT.
+        const uint64_t V = vlo | vhi | vfl | vfu;
+        int cnt = (j >= NX) ? __popcll(V) : 0;
+        int lastk = (j >= NX && V) ? (63 - __clzll(V)) * NU + ju : -1;
+        int nV = 0, last = -1;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
+          nV += __shfl(cnt, q * 16 + NX + m);
+          const int lm = __shfl(lastk, q * 16 + NX + m);
+          last = lm > last ? lm : last;
+        }
+        const bool gconv = nV == 0;
+        const bool full = (nV < best) || (pcount > 0);
+        pcount = (nV < best) ? 3 : (full ? pcount - 1 : pcount);
+        best = nV < best ? nV : best;
+        uint64_t selm = full ? V : ((last >= 0 && (last % NU) == ju && j >= NX) ? (1ull << (last / NU)) : 0ull);
+        const uint64_t nlow = (sel<NU>(low, ju) | (selm & vlo)) & ~(selm & vfl);
+        const uint64_t nup = (sel<NU>(up, ju) | (selm & vhi)) & ~(selm & vfu);
+        const bool gchanged = !gconv;
 #pragma unroll
         for (int m = 0; m < NU; ++m) {
           const int src = q * 16 + NX + m;
           const uint64_t nl = __shfl(nlow, src);
           const uint64_t nu_ = __shfl(nup, src);
-          if (!done) { low[m] = nl; up[m] = nu_; }
+          if (!done && !gconv) { low[m] = nl; up[m] = nu_; }
         }
         if (!done && !gchanged) done = true;
         const bool all_done = __all(done || !valid);

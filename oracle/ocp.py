@@ -27,7 +27,8 @@ QP solvers here:
 
 * ``riccati_solve``: Riccati recursion (HPIPM's OCP-QP structure; the QP is strictly convex so
   its minimiser is unique and method-independent).  Input boxes are handled by an exact
-  primal-dual active-set (PDAS) loop around a masked Riccati — the same algorithm the device
+  primal-dual active-set loop (with the Kim-Park block-principal-pivoting safeguard) around a
+  masked Riccati — the same algorithm the device
   runs.  HPIPM instead uses an interior-point method; both converge to the same unique
   minimiser, to within HPIPM's tolerance.  [parity unpinned: HPIPM absent]
 * ``dense_box_qp`` (tests only): condensed QP solved by SciPy BVLS, an independent exact check.
@@ -66,7 +67,7 @@ class OcpSpec:
     lbu: np.ndarray | None = None           # None -> unconstrained
     ubu: np.ndarray | None = None
     params: Params = field(default_factory=Params)
-    max_as_iter: int = 50
+    max_as_iter: int = 200
 
     def __post_init__(self):
         if self.QN is None:
@@ -176,42 +177,59 @@ def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
     return dx, du, mu, ok
 
 
-def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
-    """Primal-dual active set on input boxes around the masked Riccati.
+def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int = 3):
+    """Exact input-box QP: primal-dual active set with the Kim-Park block-principal-pivoting
+    safeguard (finite termination for the SPD reduced Hessian, a P-matrix LCP).
 
-    Returns dx, du, status, iterations.  Active sets: low = {mu + c(lb-u) > 0},
-    up = {mu + c(ub-u) < 0} with c = 1 (Hintermueller-Ito-Kunisch); converged when the sets
-    repeat, at which point the KKT conditions hold exactly.
+    Each iteration solves the equality-constrained LQ problem with the current sets (masked
+    Riccati), then collects the infeasible set V = {free u < lb} U {free u > ub} U
+    {u at lb with mu < 0} U {u at ub with mu > 0}.  |V| = 0 means the KKT conditions hold.
+    Full exchange of V while |V| keeps decreasing (or for ``pbar`` tries); otherwise only the
+    element of V with the largest index k*nu + m is exchanged (backup rule).
+    Returns dx, du, status, iterations.
     """
     Bsz, N = xbar.shape[0], spec.N
     lb = np.broadcast_to(np.asarray(spec.lbu, dtype=np.float64), (NU,))
     ub = np.broadcast_to(np.asarray(spec.ubu, dtype=np.float64), (NU,))
-    dx, du, mu, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
-    u = ubar + du
-    low = u < lb
-    up = u > ub
+    low = np.zeros((Bsz, N, NU), dtype=bool)
+    up = np.zeros((Bsz, N, NU), dtype=bool)
     done = np.zeros(Bsz, dtype=bool)
+    ok = np.ones(Bsz, dtype=bool)
     iters = np.zeros(Bsz, dtype=np.int32)
-    out_dx, out_du = dx.copy(), du.copy()
+    best = np.full(Bsz, np.iinfo(np.int32).max)
+    pcount = np.full(Bsz, pbar)
+    out_dx = np.zeros((Bsz, N + 1, NX))
+    out_du = np.zeros((Bsz, N, NU))
+    flat_idx = np.arange(N * NU).reshape(N, NU)
     for it in range(spec.max_as_iter):
         fixed = low | up
         delta = np.where(low, lb - ubar, np.where(up, ub - ubar, 0.0))
         dx, du, mu, ok2 = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, fixed, delta)
-        ok &= ok2
+        act = ~done
+        ok &= ok2 | done
+        out_dx[act], out_du[act] = dx[act], du[act]
+        iters[act] += 1
         u = ubar + du
-        mu = np.where(fixed, mu, 0.0)
-        nlow = mu + (lb - u) > 0
-        nup = mu + (ub - u) < 0
-        conv = np.all((nlow == low) & (nup == up), axis=(1, 2))
-        newly = conv & ~done
-        out_dx[newly], out_du[newly] = dx[newly], du[newly]
-        iters[~done] += 1
+        v_lo = ~fixed & (u < lb)
+        v_hi = ~fixed & (u > ub)
+        v_fl = low & (mu < 0)
+        v_fu = up & (mu > 0)
+        V = v_lo | v_hi | v_fl | v_fu
+        nV = V.sum(axis=(1, 2))
+        conv = nV == 0
         done |= conv
-        low = np.where(done[:, None, None], low, nlow)
-        up = np.where(done[:, None, None], up, nup)
         if done.all():
             break
-    out_dx[~done], out_du[~done] = dx[~done], du[~done]
+        full = (nV < best) | (pcount > 0)
+        improve = nV < best
+        pcount = np.where(improve, pbar, np.where(full, pcount - 1, pcount))
+        best = np.minimum(best, nV)
+        # backup: only the largest-index infeasible element
+        last = np.where(V, flat_idx[None], -1).reshape(Bsz, -1).max(axis=1)
+        sel = np.where(full[:, None, None], V, flat_idx[None] == last[:, None, None])
+        sel &= ~done[:, None, None]
+        low = np.where(sel & v_lo, True, np.where(sel & v_fl, False, low))
+        up = np.where(sel & v_hi, True, np.where(sel & v_fu, False, up))
     status = np.where(done, STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
     return out_dx, out_du, status, iters

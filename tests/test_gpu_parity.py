@@ -3,7 +3,8 @@
 Tolerances (north_star: 1e-5 relative in fp64):
 * fp64: per-instance ||y_dev - y_oracle||_inf / max(||y_oracle||_inf, 1) <= 1e-9 (achieved
   ~1e-12; RK4/trig rounding only).
-* fp32: the same normwise metric <= 2e-4 on X and <= 5e-4 on u0 (fp32 Riccati, SURVEY §7 ii);
+* fp32: the same normwise metric <= 5e-5 on u0, U and X (achieved ~2e-6; fp32 Riccati with a
+  symmetric-by-construction P, SURVEY §7 ii);
   the achieved numbers are printed by tests and recorded in DESIGN.md.
 """
 import os
@@ -103,7 +104,7 @@ def test_solve_matches_oracle(cfg, N, dtype, box):
     e_u, e_x, e_U = relerr(u0, o['u0']), relerr(X, o['X']), relerr(U, o['U'])
     print(f'{cfg} N={N} {dtype} box={box}: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
     assert (st == o['status']).all() and (st == 0).all()
-    tol_u, tol_x = (1e-9, 1e-9) if dtype == 'f64' else (5e-4, 2e-4)
+    tol_u, tol_x = (1e-9, 1e-9) if dtype == 'f64' else (5e-5, 5e-5)
     assert e_u.max() < tol_u and e_U.max() < tol_u and e_x.max() < tol_x
     if box:
         assert (U >= -1e-6).all() and (U <= 65 + 1e-4).all()
@@ -180,5 +181,5 @@ def test_full_size_c3_properties():
     x0 = d['x0'][idx].double().cpu().numpy()
     xr = d['xref'][idx].double().cpu().numpy()
     o = mpc_solve(x0, xr, np.full((len(idx), N, 4), np.float32(22.0725), dtype=np.float64), _spec(N))
-    assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-4
-    assert relerr(X[idx].cpu().numpy(), o['X']).max() < 2e-4
+    assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-5
+    assert relerr(X[idx].cpu().numpy(), o['X']).max() < 5e-5
