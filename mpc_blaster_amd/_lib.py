@@ -51,7 +51,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get('MPCB_LIB') or LIB_PATH
     if not os.path.exists(p):
         raise LibraryMissing(
             f'{p} not found: build it with `python -c "import __graft_entry__ as g; g.build()"` '

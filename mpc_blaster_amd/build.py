@@ -8,11 +8,13 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-SOURCES = ['mpcb_solve.hip', 'mpcb_aux.hip', 'mpcb_capi.hip']
+SOURCES = ['mpcb_solve.hip', 'mpcb_split.hip', 'mpcb_aux.hip', 'mpcb_capi.hip']
 OUT = os.path.join(HERE, 'libmpcblaster.so')
 ARCH = os.environ.get('MPCB_OFFLOAD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', f'--offload-arch={ARCH}',
+         # SLP packing into v_pk_fma_f32 bloats register pressure ~2x in these kernels
+         '-fno-slp-vectorize',
          '-Wall', '-Wno-unused-result', '-Wno-unused-variable']
 
 
@@ -25,18 +27,19 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = True, out: str | None = None, extra=()) -> str:
+    out = out or OUT
+    if out == OUT and not force and not needs_build():
         return OUT
-    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', OUT + '.tmp']
+    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', out + '.tmp']
     if verbose:
         print('[mpcb build]', ' '.join(shlex.quote(c) for c in cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f'hipcc failed ({r.returncode})')
-    os.replace(OUT + '.tmp', OUT)
-    return OUT
+    os.replace(out + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':

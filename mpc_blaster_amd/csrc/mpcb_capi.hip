@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -55,9 +56,12 @@ struct mpcb_handle {
   int64_t max_batch;
   int grid;              // resident slots (one wavefront of GROUPS instances each)
   void* weights;         // Weights<T>
-  void* scratch;
+  void* scratch;          // box path: per-slot workspace of the fused kernel
   int64_t slot_elems;
   int64_t scratch_bytes;
+  int split;              // 1: three-kernel split path; 0: fused single kernel
+  int64_t chunk;          // split path: instances per chunk
+  int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
   Model<float> Mf;
 };
@@ -126,9 +130,27 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   int64_t grid = (int64_t)prop.multiProcessorCount * 16;
   if (grid > waves_needed) grid = waves_needed;
   h->grid = (int)grid;
-  h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
   const size_t esz = f64 ? sizeof(double) : sizeof(float);
-  h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
+  // Path: the split kernels (thread-per-instance rollout/forward passes) need a large batch
+  // to fill 1024 SIMDs; small batches and the input-box active-set loop use the fused kernel.
+  int64_t split_min = 16384;
+  if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
+  h->split = (!cfg->box_u && max_batch >= split_min) ? 1 : 0;
+  if (!h->split) {
+    h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
+    h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
+  } else {
+    // chunk of instances whose intermediates (~N*160 scalars each) stay near the 256 MiB
+    // Infinity Cache while still giving the Riccati kernel >= 4 wavefronts per SIMD
+    int64_t chunk = 65536;
+    if (const char* e = getenv("MPCB_CHUNK")) chunk = atoll(e);
+    if (chunk < 64) chunk = 64;
+    if (chunk > max_batch) chunk = max_batch;
+    h->chunk = chunk;
+    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1) : split_elems_per_instance<float>(cfg->N, 1);
+    h->chunk_elems = per * ((chunk + 3) / 4 * 4);
+    h->scratch_bytes = h->chunk_elems * (int64_t)esz;
+  }
   fill_model(*cfg, Jinv, h->Md);
   fill_model(*cfg, Jinv, h->Mf);
   hipError_t e = hipMalloc(&h->scratch, (size_t)h->scratch_bytes);
@@ -176,6 +198,37 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
                       const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
                       const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                       void* u0, void* X, void* U, int32_t* status, void* stream) {
+  if (h->split) {
+    SplitArgs<T> a;
+    a.N = h->cfg.N;
+    a.mode = mode;
+    a.h = (T)h->cfg.dt;
+    a.s = (T)h->cfg.cost_scale;
+    if constexpr (sizeof(T) == 8) a.M = h->Md; else a.M = h->Mf;
+    a.W = reinterpret_cast<const Weights<T>*>(h->weights);
+    a.x0 = (const T*)x0; a.x0_sb = x0_sb;
+    a.xref = (const T*)xref; a.xref_sb = xref_sb;
+    a.uref = (const T*)uref; a.uref_sb = uref_sb;
+    a.wind = (const T*)wind; a.wind_sb = wind_sb;
+    a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
+    a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
+    a.fwd = (X || U || mode == MPCB_MODE_ITERATE) ? 1 : 0;
+    const int N = h->cfg.N;
+    for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
+      const int64_t nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
+      T* base = (T*)h->scratch;
+      a.b0 = b0;
+      a.nb = nb;
+      const int64_t nbp = (nb + 3) / 4 * 4;   // quad-blocked layout pads to 4 instances
+      a.XU = base;
+      a.CC = a.XU + (int64_t)(N + 1) * nbp * XU_REC;
+      a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
+      a.GP = a.KR + (int64_t)N * nbp * KR_REC;
+      hipError_t e = launch_split<T>(a, (hipStream_t)stream);
+      if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));
+    }
+    return MPCB_OK;
+  }
   SolveArgs<T> a;
   a.B = B;
   a.N = h->cfg.N;

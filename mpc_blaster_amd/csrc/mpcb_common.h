@@ -1,0 +1,91 @@
+// mpcb_common.h — device helpers shared by the solve kernels (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcb_kernels.h"
+
+namespace mpcb {
+
+template <class T>
+struct GroupLds {
+  T P[NX * NX];   // value-function Hessian, P[l*NX + i] = column l (symmetric)
+  T X[NZ * NX];   // X[j*NX + i] = ([A|B])_{i j}
+  T Hu[NZ * NU];  // Hu[j*NU + m] = G_{NX+m, j}   (H_ux columns, then H_uu)
+  T v[NZ];        // vector exchange (e = ybar - yref, then pt = p + P b)
+  T hv[NZ];       // gradient h = [h_x; h_u]
+};
+
+// Per-lane record in the workspace, per stage: 4 gain values (+ box-mode extras).
+template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
+
+// Identity that LLVM cannot see through (keeps selects of array elements as selects).
+template <class T> __device__ __forceinline__ T opq(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// a[j] (0 <= j < 16, n <= 16) for a register array, as a bit-tree of selects.  Without the
+// opaque copies InstCombine folds select(load a[i], load a[k]) into a load from a selected
+// address, which turns the register array into a dynamically indexed scratch array.
+template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
+  T l0[8], l1[4], l2[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const T lo = opq(a[(2 * i < n) ? 2 * i : n - 1]);
+    const T hi = opq(a[(2 * i + 1 < n) ? 2 * i + 1 : n - 1]);
+    l0[i] = (j & 1) ? hi : lo;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) l1[i] = (j & 2) ? opq(l0[2 * i + 1]) : opq(l0[2 * i]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) l2[i] = (j & 4) ? opq(l1[2 * i + 1]) : opq(l1[2 * i]);
+  return (j & 8) ? opq(l2[1]) : opq(l2[0]);
+}
+
+template <class T>
+__device__ __forceinline__ void chol4(const T H[16], T L[10]) {
+  // L packed lower: L00 L10 L11 L20 L21 L22 L30 L31 L32 L33 (diagonal holds 1/L_ii)
+  T l00 = sqrt(H[0]);
+  T i00 = T(1) / l00;
+  T l10 = H[4] * i00, l20 = H[8] * i00, l30 = H[12] * i00;
+  T l11 = sqrt(H[5] - l10 * l10);
+  T i11 = T(1) / l11;
+  T l21 = (H[9] - l20 * l10) * i11, l31 = (H[13] - l30 * l10) * i11;
+  T l22 = sqrt(H[10] - l20 * l20 - l21 * l21);
+  T i22 = T(1) / l22;
+  T l32 = (H[14] - l30 * l20 - l31 * l21) * i22;
+  T l33 = sqrt(H[15] - l30 * l30 - l31 * l31 - l32 * l32);
+  T i33 = T(1) / l33;
+  L[0] = i00; L[1] = l10; L[2] = i11; L[3] = l20; L[4] = l21; L[5] = i22;
+  L[6] = l30; L[7] = l31; L[8] = l32; L[9] = i33;
+}
+
+template <class T>
+__device__ __forceinline__ void chol4_solve(const T L[10], const T b[4], T x[4]) {
+  // forward L y = b, backward L^T x = y
+  T y0 = b[0] * L[0];
+  T y1 = (b[1] - L[1] * y0) * L[2];
+  T y2 = (b[2] - L[3] * y0 - L[4] * y1) * L[5];
+  T y3 = (b[3] - L[6] * y0 - L[7] * y1 - L[8] * y2) * L[9];
+  x[3] = y3 * L[9];
+  x[2] = (y2 - L[8] * x[3]) * L[5];
+  x[1] = (y1 - L[4] * x[2] - L[7] * x[3]) * L[2];
+  x[0] = (y0 - L[1] * x[1] - L[3] * x[2] - L[6] * x[3]) * L[0];
+}
+
+template <int n, class T>
+__device__ __forceinline__ void store_vec(T* __restrict__ p, const T* v) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) p[i] = v[i];
+}
+
+// per (interval, instance) record: 80 linearisation scalars, 12 gap values, 4 pad
+constexpr int CC_REC = LIN_STAGE + 16;
+
+template <int n, class T>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, T* out) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) out[i] = p[i];
+}
+
+}  // namespace mpcb

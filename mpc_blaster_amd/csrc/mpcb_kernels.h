@@ -44,6 +44,39 @@ struct SolveArgs {
 };
 
 template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipStream_t st);
+
+// Split (unconstrained) path: three launches per chunk of instances.
+//   P1 nominal  (thread / instance): rollout or iterate, captures linearisation scalars
+//   P2 riccati  (16 lanes / instance): tangent columns of [A|B] + Riccati, writes gains
+//   P3 forward  (thread / instance): dx/du propagation (RK4 JVP), writes u0, X, U, status
+// Chunk workspace layouts, structure-of-arrays blocked by instance quads (mpcb_split.hip soa();
+// c = chunk-local instance, nb = chunk size rounded up to a multiple of 4):
+//   XU [(N+1)][16][nb]  xbar_k | ubar_k
+//   CC [N][80][nb]      4 RK stages x 20 linearisation scalars
+//   GP [N][12][nb]      gap Phi(xbar_k, ubar_k) - xbar_{k+1}      (iterate mode only)
+//   KR [N][52][nb]      K_k (48, K[m][i] at row 4*i+m) | kff_k (4)
+constexpr int XU_REC = 16, CCS_REC = 80, GP_REC = 12, KR_REC = 52;
+
+template <class T>
+struct SplitArgs {
+  int64_t b0;        // first global instance of the chunk
+  int64_t nb;        // instances in the chunk
+  int N;
+  int mode;
+  T h, s;
+  Model<T> M;
+  const Weights<T>* W;
+  const T* x0; int64_t x0_sb;
+  const T* xref; int64_t xref_sb;
+  const T* uref; int64_t uref_sb;
+  const T* wind; int64_t wind_sb;
+  const T* xbar; const T* ubar;
+  T* u0; T* X; T* U; int32_t* status;
+  T* XU; T* CC; T* GP; T* KR;
+  int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
+};
+template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st);
+template <class T> int64_t split_elems_per_instance(int N, int iterate);  // per 64-padded instance
 template <class T> int64_t solve_slot_elems(int N, int box);
 
 template <class T>

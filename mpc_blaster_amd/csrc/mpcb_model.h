@@ -149,3 +149,165 @@ __device__ __forceinline__ void rk4(const T* __restrict__ x, const T* __restrict
 }
 
 }  // namespace mpcb
+
+namespace mpcb {
+
+// ---------------------------------------------------------------------------------------------
+// Split evaluation used by the fused solve kernel.  The nominal pass evaluates f once per RK4
+// stage and captures the 20 scalars the tangent needs (trig values, rotation column, thrust
+// scale, angular momentum, body rates): ``Lin``.  The tangent passes then apply J_f(x_i,u)·(dx,du)
+// from those scalars with ~70 FMAs and no transcendental, so every direction lane carries only
+// tangent vectors (register diet: the 16 lanes of an instance no longer recompute the shared
+// nominal trajectory, its sin/cos, or hold it live).
+// ---------------------------------------------------------------------------------------------
+constexpr int LIN_N = 20;      // scalars per RK4 stage
+constexpr int LIN_STAGE = 80;  // per shooting interval (4 stages)
+
+template <class T>
+__device__ __forceinline__ void f_nom_lin(const T* __restrict__ x, const T* __restrict__ u,
+                                          const Model<T>& M, const T w[3], T* __restrict__ f,
+                                          T* __restrict__ c) {
+  T sf, cf, st, ct, sp, cp;
+  sc(x[3], &sf, &cf);
+  sc(x[4], &st, &ct);
+  sc(x[5], &sp, &cp);
+  const T ict = T(1) / ct;
+  const T tt = st * ict;
+  const T wx = x[9], wy = x[10], wz = x[11];
+  f[0] = x[6]; f[1] = x[7]; f[2] = x[8];
+  const T a = sf * wy + cf * wz;
+  const T b = cf * wy - sf * wz;
+  f[3] = wx + tt * a;
+  f[4] = b;
+  f[5] = a * ict;
+  const T Ttot = (u[0] + u[1]) + (u[2] + u[3]) + M.t_blast;
+  const T s = Ttot * M.minv;
+  const T cfst = cf * st;
+  const T r0 = cp * cfst + sp * sf;
+  const T r1 = sp * cfst - cp * sf;
+  const T r2 = cf * ct;
+  f[6] = r0 * s + w[0] * M.minv;
+  f[7] = r1 * s + w[1] * M.minv;
+  f[8] = r2 * s - M.g + w[2] * M.minv;
+  const T jw0 = M.J[0] * wx + M.J[1] * wy + M.J[2] * wz;
+  const T jw1 = M.J[3] * wx + M.J[4] * wy + M.J[5] * wz;
+  const T jw2 = M.J[6] * wx + M.J[7] * wy + M.J[8] * wz;
+  const T c0 = wy * jw2 - wz * jw1;
+  const T c1 = wz * jw0 - wx * jw2;
+  const T c2 = wx * jw1 - wy * jw0;
+  const T m0 = (u[1] + u[3] - u[0] - u[2]) * M.ly - c0;
+  const T m1 = (u[1] + u[2] - u[0] - u[3]) * M.lx - c1;
+  const T m2 = (u[2] + u[3] - u[0] - u[1]) * M.c - c2;
+  f[9] = M.Jinv[0] * m0 + M.Jinv[1] * m1 + M.Jinv[2] * m2;
+  f[10] = M.Jinv[3] * m0 + M.Jinv[4] * m1 + M.Jinv[5] * m2;
+  f[11] = M.Jinv[6] * m0 + M.Jinv[7] * m1 + M.Jinv[8] * m2;
+  c[0] = sf; c[1] = cf; c[2] = st; c[3] = ct; c[4] = sp; c[5] = cp; c[6] = ict; c[7] = tt;
+  c[8] = a; c[9] = cfst; c[10] = s; c[11] = r0; c[12] = r1; c[13] = r2;
+  c[14] = jw0; c[15] = jw1; c[16] = jw2; c[17] = wx; c[18] = wy; c[19] = wz;
+}
+
+// df = J_f(x_i, u) · (dx, du) from the captured scalars c (same algebra as f_tan's TAN branch).
+template <class T>
+__device__ __forceinline__ void f_tan_lin(const T* __restrict__ c, const T* __restrict__ dx,
+                                          const T* __restrict__ du, const Model<T>& M,
+                                          T* __restrict__ df) {
+  const T sf = c[0], cf = c[1], st = c[2], ct = c[3], sp = c[4], cp = c[5], ict = c[6], tt = c[7];
+  const T a = c[8], cfst = c[9], s = c[10], r0 = c[11], r1 = c[12], r2 = c[13];
+  const T jw0 = c[14], jw1 = c[15], jw2 = c[16], wx = c[17], wy = c[18], wz = c[19];
+  const T dphi = dx[3], dth = dx[4], dpsi = dx[5];
+  const T dwx = dx[9], dwy = dx[10], dwz = dx[11];
+  const T dsf = cf * dphi, dcf = -sf * dphi;
+  const T dst = ct * dth, dct = -st * dth;
+  const T dsp = cp * dpsi, dcp = -sp * dpsi;
+  const T dict = -ict * ict * dct;
+  const T dtt = dst * ict + st * dict;
+  df[0] = dx[6]; df[1] = dx[7]; df[2] = dx[8];
+  const T da = dsf * wy + sf * dwy + dcf * wz + cf * dwz;
+  const T db = dcf * wy + cf * dwy - dsf * wz - sf * dwz;
+  df[3] = dwx + dtt * a + tt * da;
+  df[4] = db;
+  df[5] = da * ict + a * dict;
+  const T dT = (du[0] + du[1]) + (du[2] + du[3]);
+  const T ds = dT * M.minv;
+  const T dcfst = dcf * st + cf * dst;
+  const T dr0 = dcp * cfst + cp * dcfst + dsp * sf + sp * dsf;
+  const T dr1 = dsp * cfst + sp * dcfst - dcp * sf - cp * dsf;
+  const T dr2 = dcf * ct + cf * dct;
+  df[6] = dr0 * s + r0 * ds;
+  df[7] = dr1 * s + r1 * ds;
+  df[8] = dr2 * s + r2 * ds;
+  const T djw0 = M.J[0] * dwx + M.J[1] * dwy + M.J[2] * dwz;
+  const T djw1 = M.J[3] * dwx + M.J[4] * dwy + M.J[5] * dwz;
+  const T djw2 = M.J[6] * dwx + M.J[7] * dwy + M.J[8] * dwz;
+  const T dc0 = dwy * jw2 + wy * djw2 - dwz * jw1 - wz * djw1;
+  const T dc1 = dwz * jw0 + wz * djw0 - dwx * jw2 - wx * djw2;
+  const T dc2 = dwx * jw1 + wx * djw1 - dwy * jw0 - wy * djw0;
+  const T dm0 = (du[1] + du[3] - du[0] - du[2]) * M.ly - dc0;
+  const T dm1 = (du[1] + du[2] - du[0] - du[3]) * M.lx - dc1;
+  const T dm2 = (du[2] + du[3] - du[0] - du[1]) * M.c - dc2;
+  df[9] = M.Jinv[0] * dm0 + M.Jinv[1] * dm1 + M.Jinv[2] * dm2;
+  df[10] = M.Jinv[3] * dm0 + M.Jinv[4] * dm1 + M.Jinv[5] * dm2;
+  df[11] = M.Jinv[6] * dm0 + M.Jinv[7] * dm1 + M.Jinv[8] * dm2;
+}
+
+// Nominal RK4 step that hands each stage's captured scalars to ``sink(stage, c)``.
+template <class T, class Sink>
+__device__ __forceinline__ void rk4_nom(const T* __restrict__ x, const T* __restrict__ u, T h,
+                                        const Model<T>& M, const T w[3], T* __restrict__ xn,
+                                        Sink&& sink) {
+  constexpr int NX = 12;
+  T k[NX], xs[NX], c[LIN_N];
+  const T h2 = T(0.5) * h, h6 = h / T(6);
+  f_nom_lin<T>(x, u, M, w, k, c);
+  sink(0, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] = k[i]; xs[i] = x[i] + h2 * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c);
+  sink(1, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; xs[i] = x[i] + h2 * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c);
+  sink(2, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; xs[i] = x[i] + h * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c);
+  sink(3, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xn[i] = x[i] + h6 * (xn[i] + k[i]);
+}
+
+// Tangent of the RK4 step along (dx, du) from the 4 captured stages at ``C`` (LIN_STAGE values).
+// ``cs`` is the element stride of C (1 for an AoS record, the chunk size for SoA layouts).
+template <class T>
+__device__ __forceinline__ void rk4_tan(const T* __restrict__ C, const T* __restrict__ dx,
+                                        const T* __restrict__ du, T h, const Model<T>& M,
+                                        T* __restrict__ dxn, int64_t cs = 1) {
+  constexpr int NX = 12;
+  T dk[NX], dxs[NX], c[LIN_N];
+  const T h2 = T(0.5) * h, h6 = h / T(6);
+#pragma unroll
+  for (int i = 0; i < LIN_N; ++i) c[i] = C[(i) * cs];
+  f_tan_lin<T>(c, dx, du, M, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+#pragma unroll
+  for (int i = 0; i < LIN_N; ++i) c[i] = C[(LIN_N + i) * cs];
+  f_tan_lin<T>(c, dxs, du, M, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+#pragma unroll
+  for (int i = 0; i < LIN_N; ++i) c[i] = C[(2 * LIN_N + i) * cs];
+  f_tan_lin<T>(c, dxs, du, M, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
+  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+#pragma unroll
+  for (int i = 0; i < LIN_N; ++i) c[i] = C[(3 * LIN_N + i) * cs];
+  f_tan_lin<T>(c, dxs, du, M, dk);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) dxn[i] = dx[i] + h6 * (dxn[i] + dk[i]);
+}
+
+}  // namespace mpcb

@@ -23,86 +23,13 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/mpcb.h"
-#include "mpcb_kernels.h"
+#include "mpcb_common.h"
 
 #ifndef MPCB_WAVES
 #define MPCB_WAVES
 #endif
 
 namespace mpcb {
-
-template <class T>
-struct GroupLds {
-  T P[NX * NX];   // value-function Hessian, P[l*NX + i] = column l (symmetric)
-  T X[NZ * NX];   // X[j*NX + i] = ([A|B])_{i j}
-  T Hu[NZ * NU];  // Hu[j*NU + m] = G_{NX+m, j}   (H_ux columns, then H_uu)
-  T v[NZ];        // vector exchange (e = ybar - yref, then pt = p + P b)
-  T hv[NZ];       // gradient h = [h_x; h_u]
-};
-
-// Per-lane record in the workspace, per stage: 4 gain values (+ box-mode extras).
-template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
-
-// Identity that LLVM cannot see through (keeps selects of array elements as selects).
-template <class T> __device__ __forceinline__ T opq(T x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
-// a[j] (0 <= j < 16, n <= 16) for a register array, as a bit-tree of selects.  Without the
-// opaque copies InstCombine folds select(load a[i], load a[k]) into a load from a selected
-// address, which turns the register array into a dynamically indexed scratch array.
-template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
-  T l0[8], l1[4], l2[2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const T lo = opq(a[(2 * i < n) ? 2 * i : n - 1]);
-    const T hi = opq(a[(2 * i + 1 < n) ? 2 * i + 1 : n - 1]);
-    l0[i] = (j & 1) ? hi : lo;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) l1[i] = (j & 2) ? opq(l0[2 * i + 1]) : opq(l0[2 * i]);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) l2[i] = (j & 4) ? opq(l1[2 * i + 1]) : opq(l1[2 * i]);
-  return (j & 8) ? opq(l2[1]) : opq(l2[0]);
-}
-
-template <class T>
-__device__ __forceinline__ void chol4(const T H[16], T L[10]) {
-  // L packed lower: L00 L10 L11 L20 L21 L22 L30 L31 L32 L33 (diagonal holds 1/L_ii)
-  T l00 = sqrt(H[0]);
-  T i00 = T(1) / l00;
-  T l10 = H[4] * i00, l20 = H[8] * i00, l30 = H[12] * i00;
-  T l11 = sqrt(H[5] - l10 * l10);
-  T i11 = T(1) / l11;
-  T l21 = (H[9] - l20 * l10) * i11, l31 = (H[13] - l30 * l10) * i11;
-  T l22 = sqrt(H[10] - l20 * l20 - l21 * l21);
-  T i22 = T(1) / l22;
-  T l32 = (H[14] - l30 * l20 - l31 * l21) * i22;
-  T l33 = sqrt(H[15] - l30 * l30 - l31 * l31 - l32 * l32);
-  T i33 = T(1) / l33;
-  L[0] = i00; L[1] = l10; L[2] = i11; L[3] = l20; L[4] = l21; L[5] = i22;
-  L[6] = l30; L[7] = l31; L[8] = l32; L[9] = i33;
-}
-
-template <class T>
-__device__ __forceinline__ void chol4_solve(const T L[10], const T b[4], T x[4]) {
-  // forward L y = b, backward L^T x = y
-  T y0 = b[0] * L[0];
-  T y1 = (b[1] - L[1] * y0) * L[2];
-  T y2 = (b[2] - L[3] * y0 - L[4] * y1) * L[5];
-  T y3 = (b[3] - L[6] * y0 - L[7] * y1 - L[8] * y2) * L[9];
-  x[3] = y3 * L[9];
-  x[2] = (y2 - L[8] * x[3]) * L[5];
-  x[1] = (y1 - L[4] * x[2] - L[7] * x[3]) * L[2];
-  x[0] = (y0 - L[1] * x[1] - L[3] * x[2] - L[6] * x[3]) * L[0];
-}
-
-template <int n, class T>
-__device__ __forceinline__ void load_vec(const T* __restrict__ p, T* out) {
-#pragma unroll
-  for (int i = 0; i < n; ++i) out[i] = p[i];
-}
 
 template <class T, int BOX>
 __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
@@ -120,7 +47,8 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
   T* slot = a.scratch + (int64_t)blockIdx.x * a.slot_elems;
   T* XU = slot;                                        // [(N+1)][64]       xbar | ubar
-  T* KR = slot + (int64_t)(N + 1) * 64;                // [N][64][RN]       gains (+box extras)
+  T* CC = XU + (int64_t)(N + 1) * 64;                  // [N][GROUPS][CC_REC] lin. scalars | gap
+  T* KR = CC + (int64_t)N * GROUPS * CC_REC;           // [N][64][RN]       gains (+box extras)
 
   for (int64_t wave = blockIdx.x; wave * GROUPS < a.B; wave += gridDim.x) {
     const int64_t b_raw = wave * GROUPS + q;
@@ -136,26 +64,43 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
     const T* ur = a.uref + b * a.uref_sb;
     const T* x0p = a.x0 + b * a.x0_sb;
 
-    // ------------------------------------------------------------------ pass 1: iterate
-    if (!iterate) {
-      T xb[NX], ub[NU];
-      load_vec<NX>(x0p, xb);
-      for (int k = 0; k < N; ++k) {
-        load_vec<NU>(ur + (int64_t)k * NU, ub);
-        XU[(int64_t)k * 64 + lane] = (j < NX) ? sel<NX>(xb, j) : sel<NU>(ub, ju);
-        T xn[NX], dd[1];
-        rk4<T, false>(xb, nullptr, ub, nullptr, a.h, a.M, w, xn, dd);
-#pragma unroll
-        for (int i = 0; i < NX; ++i) xb[i] = xn[i];
-      }
-      XU[(int64_t)N * 64 + lane] = (j < NX) ? sel<NX>(xb, j) : T(0);
-    } else {
+    // ------------------------------------------------------------------ pass 1: nominal
+    // Every lane of the group integrates the same nominal trajectory; lane 0 of the group
+    // publishes xbar/ubar (XU), the 80 captured linearisation scalars per interval and the gap
+    // (CC).  ROLLOUT: xbar = RK4 rollout of u_ref from x0 (gap 0).  ITERATE: the given iterate.
+    {
       const T* xbp = a.xbar + b * (int64_t)(N + 1) * NX;
       const T* ubp = a.ubar + b * (int64_t)N * NU;
-      for (int k = 0; k <= N; ++k) {
-        const T vx = xbp[(int64_t)k * NX + jx];
-        const T vu = (k < N) ? ubp[(int64_t)k * NU + ju] : T(0);
-        XU[(int64_t)k * 64 + lane] = (j < NX) ? vx : vu;
+      T xb[NX], ub[NU];
+      load_vec<NX>(iterate ? xbp : x0p, xb);
+      for (int k = 0; k < N; ++k) {
+        if (iterate) load_vec<NX>(xbp + (int64_t)k * NX, xb);
+        load_vec<NU>(iterate ? ubp + (int64_t)k * NU : ur + (int64_t)k * NU, ub);
+        T* cc = CC + ((int64_t)k * GROUPS + q) * CC_REC;
+        if (j == 0) {
+          store_vec<NX>(XU + (int64_t)k * 64 + q * 16, xb);
+          store_vec<NU>(XU + (int64_t)k * 64 + q * 16 + NX, ub);
+        }
+        T xn[NX];
+        rk4_nom<T>(xb, ub, a.h, a.M, w, xn, [&](int stage, const T* c) {
+          if (j == 0) store_vec<LIN_N>(cc + stage * LIN_N, c);
+        });
+        if (iterate) {
+          T gp[NX];
+          const T* nx = xbp + (int64_t)(k + 1) * NX;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) gp[i] = xn[i] - nx[i];
+          if (j == 0) store_vec<NX>(cc + LIN_STAGE, gp);
+        } else {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) xb[i] = xn[i];
+        }
+      }
+      if (iterate) load_vec<NX>(xbp + (int64_t)N * NX, xb);
+      if (j == 0) {
+        store_vec<NX>(XU + (int64_t)N * 64 + q * 16, xb);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) XU[(int64_t)N * 64 + q * 16 + NX + m] = T(0);
       }
     }
     __syncthreads();
@@ -189,26 +134,22 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
       for (int k = N - 1; k >= 0; --k) {
         T col[NX];
         {
-          T xb[NX], ub[NU];
-          const T* p = XU + (int64_t)k * 64 + q * 16;
-          load_vec<NX>(p, xb);
-          load_vec<NU>(p + NX, ub);
+          const T* cc = CC + ((int64_t)k * GROUPS + q) * CC_REC;
           // e = ybar - yref (component j), exchanged through LDS for block-diagonal W
           const T ybar = XU[(int64_t)k * 64 + lane];
           L.v[j] = ybar - ((j < NX) ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
-          // tangent RK4: column j of [A|B]
-          T dx[NX], du[NU], phi[NX];
+          // tangent RK4 seeded with e_j: column j of [A|B]
+          T dx[NX], du[NU];
 #pragma unroll
           for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
 #pragma unroll
           for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
-          rk4<T, true>(xb, dx, ub, du, a.h, a.M, w, phi, col);
+          rk4_tan<T>(cc, dx, du, a.h, a.M, col);
           // gap b = Phi(xbar_k, ubar_k) - xbar_{k+1};  pt = p + P b  (P symmetric: row j = col j)
           T pt = pj;
           if (iterate) {
-            const T* pn = XU + (int64_t)(k + 1) * 64 + q * 16;
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pt += L.P[jx * NX + i] * (phi[i] - pn[i]);
+            for (int i = 0; i < NX; ++i) pt += L.P[jx * NX + i] * cc[LIN_STAGE + i];
           }
           L.hv[j] = pt;
         }
@@ -379,10 +320,8 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
 #pragma unroll
             for (int m = 0; m < NU; ++m) duk[m] += r[m] * dxk[l];
           }
-          T xb[NX], ub[NU];
-          const T* p = XU + (int64_t)k * 64 + q * 16;
-          load_vec<NX>(p, xb);
-          load_vec<NU>(p + NX, ub);
+          T ub[NU];
+          load_vec<NU>(XU + (int64_t)k * 64 + q * 16 + NX, ub);
           if (k == 0) {
 #pragma unroll
             for (int m = 0; m < NU; ++m) u0v[m] = ub[m] + duk[m];
@@ -406,15 +345,16 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
             }
           }
           if (write) {
-            if (a.X && j < NX) a.X[(b * (N + 1) + k) * NX + j] = sel<NX>(xb, j) + sel<NX>(dxk, j);
-            if (a.U && j >= NX) a.U[(b * N + k) * NU + ju] = sel<NU>(ub, ju) + sel<NU>(duk, ju);
+            const T ybar = XU[(int64_t)k * 64 + lane];
+            if (a.X && j < NX) a.X[(b * (N + 1) + k) * NX + j] = ybar + sel<NX>(dxk, j);
+            if (a.U && j >= NX) a.U[(b * N + k) * NU + ju] = ybar + sel<NU>(duk, ju);
           }
-          T phi[NX], dphi[NX];
-          rk4<T, true>(xb, dxk, ub, duk, a.h, a.M, w, phi, dphi);
+          const T* cc = CC + ((int64_t)k * GROUPS + q) * CC_REC;
+          T dphi[NX];
+          rk4_tan<T>(cc, dxk, duk, a.h, a.M, dphi);
           if (iterate) {
-            const T* pn = XU + (int64_t)(k + 1) * 64 + q * 16;
 #pragma unroll
-            for (int i = 0; i < NX; ++i) dxk[i] = dphi[i] + (phi[i] - pn[i]);
+            for (int i = 0; i < NX; ++i) dxk[i] = dphi[i] + cc[LIN_STAGE + i];
           } else {
 #pragma unroll
             for (int i = 0; i < NX; ++i) dxk[i] = dphi[i];
@@ -487,7 +427,7 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
 
 template <class T> int64_t solve_slot_elems(int N, int box) {
   const int RN = box ? Rec<1>::n : Rec<0>::n;
-  return (int64_t)(N + 1) * 64 + (int64_t)N * 64 * RN;
+  return (int64_t)(N + 1) * 64 + (int64_t)N * GROUPS * CC_REC + (int64_t)N * 64 * RN;
 }
 
 template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipStream_t st) {

@@ -23,11 +23,21 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 
 
-def _mpc(N, dtype='f64', box=False, max_batch=4096, **kw):
+def _mpc(N, dtype='f64', box=False, max_batch=4096, path=None, **kw):
+    """path: None (library default by batch size), 'split' or 'fused' (forced via env)."""
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     cfg = MPCConfig(N=N, dtype=dtype, lbu=np.zeros(4) if box else None,
                     ubu=np.full(4, 65.0) if box else None, **kw)
-    return BatchedMPC(cfg, max_batch=max_batch)
+    old = os.environ.get('MPCB_SPLIT_MIN_BATCH')
+    if path is not None:
+        os.environ['MPCB_SPLIT_MIN_BATCH'] = '1' if path == 'split' else str(1 << 40)
+    try:
+        return BatchedMPC(cfg, max_batch=max_batch)
+    finally:
+        if old is None:
+            os.environ.pop('MPCB_SPLIT_MIN_BATCH', None)
+        else:
+            os.environ['MPCB_SPLIT_MIN_BATCH'] = old
 
 
 def _spec(N, box=False):
@@ -84,14 +94,17 @@ def test_c1_golden_fp64():
     assert m.get_status().cpu().numpy().tolist() == [0]
 
 
-@pytest.mark.parametrize('cfg,N,dtype,box', [
-    ('c2', 20, 'f64', False), ('c3', 20, 'f64', False), ('c3', 20, 'f32', False),
-    ('c4', 30, 'f64', True), ('c4', 30, 'f32', True), ('c2', 10, 'f32', False),
+@pytest.mark.parametrize('cfg,N,dtype,box,path', [
+    ('c2', 20, 'f64', False, 'fused'), ('c3', 20, 'f64', False, 'fused'),
+    ('c3', 20, 'f32', False, 'fused'), ('c2', 10, 'f32', False, 'fused'),
+    ('c2', 20, 'f64', False, 'split'), ('c3', 20, 'f64', False, 'split'),
+    ('c3', 20, 'f32', False, 'split'), ('c2', 10, 'f32', False, 'split'),
+    ('c4', 30, 'f64', True, None), ('c4', 30, 'f32', True, None),
 ])
-def test_solve_matches_oracle(cfg, N, dtype, box):
+def test_solve_matches_oracle(cfg, N, dtype, box, path):
     B = 203   # ragged: not a multiple of the 4-instance wave
     inp = make_inputs(cfg, ids=np.arange(B, dtype=np.uint64), N=N)
-    m = _mpc(N, dtype, box, max_batch=B)
+    m = _mpc(N, dtype, box, max_batch=B, path=path)
     m.solve(inp['x0'], inp['xref'], inp['uref'])
     torch.cuda.synchronize()
     u0 = m.get_control().cpu().numpy()
@@ -102,7 +115,7 @@ def test_solve_matches_oracle(cfg, N, dtype, box):
     cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
     o = mpc_solve(cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), _spec(N, box))
     e_u, e_x, e_U = relerr(u0, o['u0']), relerr(X, o['X']), relerr(U, o['U'])
-    print(f'{cfg} N={N} {dtype} box={box}: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
+    print(f'{cfg} N={N} {dtype} box={box} path={path}: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
     assert (st == o['status']).all() and (st == 0).all()
     tol_u, tol_x = (1e-9, 1e-9) if dtype == 'f64' else (5e-5, 5e-5)
     assert e_u.max() < tol_u and e_U.max() < tol_u and e_x.max() < tol_x
@@ -110,14 +123,15 @@ def test_solve_matches_oracle(cfg, N, dtype, box):
         assert (U >= -1e-6).all() and (U <= 65 + 1e-4).all()
 
 
-def test_iterate_mode_matches_oracle_fp64():
+@pytest.mark.parametrize('path', ['fused', 'split'])
+def test_iterate_mode_matches_oracle_fp64(path):
     """acados SQP_RTI semantics: linearise at a given iterate with gaps and dx0 != 0."""
     N, B = 12, 41
     rng = np.random.default_rng(9)
     inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
     xbar = inp['xref'] + rng.normal(scale=0.05, size=(B, N + 1, 12))
     ubar = inp['uref'] + rng.normal(scale=1.0, size=(B, N, 4))
-    m = _mpc(N, 'f64', max_batch=B)
+    m = _mpc(N, 'f64', max_batch=B, path=path)
     m.solve_iterate(inp['x0'], xbar, ubar, inp['xref'], inp['uref'])
     torch.cuda.synchronize()
     o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], _spec(N), mode='iterate', xbar=xbar, ubar=ubar)
@@ -125,10 +139,11 @@ def test_iterate_mode_matches_oracle_fp64():
     assert relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max() < 1e-9
 
 
-def test_wind_extension_fp64():
+@pytest.mark.parametrize('path', ['fused', 'split'])
+def test_wind_extension_fp64(path):
     N, B = 8, 16
     inp = make_inputs('c5', ids=np.arange(B, dtype=np.uint64), N=N)
-    m = _mpc(N, 'f64', max_batch=B)
+    m = _mpc(N, 'f64', max_batch=B, path=path)
     m.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'])
     torch.cuda.synchronize()
     o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], _spec(N), wind=inp['wind'])
@@ -149,10 +164,11 @@ def test_sim_step_and_histogram():
     assert np.array_equal(counts, ref)
 
 
-def test_u0_only_path_equals_full_path():
+@pytest.mark.parametrize('path', ['fused', 'split'])
+def test_u0_only_path_equals_full_path(path):
     N, B = 20, 64
     inp = make_inputs('c3', ids=np.arange(B, dtype=np.uint64), N=N)
-    m = _mpc(N, 'f32', max_batch=B)
+    m = _mpc(N, 'f32', max_batch=B, path=path)
     a = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=False).clone()
     b = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=True)
     torch.cuda.synchronize()
