@@ -77,8 +77,11 @@ int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_hand
 int mpcb_destroy(mpcb_handle* h);
 const char* mpcb_last_error(void);
 int mpcb_abi_version(void);
-/* Number of instances currently processed concurrently per launch (informational). */
+/* Workspace bytes owned by the handle (informational). */
 int64_t mpcb_workspace_bytes(const mpcb_handle* h);
+/* Kernel path chosen at creation: 0 = fused single kernel (small batches, input boxes),
+ * 1 = split nominal / Riccati / forward kernels (large unconstrained batches). */
+int mpcb_path(const mpcb_handle* h);
 
 /*
  * One SQP_RTI step for B independent instances, linearised at the RK4 rollout of u_ref from

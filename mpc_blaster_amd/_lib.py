@@ -17,7 +17,7 @@ MPCB_MAX_NX, MPCB_MAX_NU = 17, 6
 STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
 
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
-           'mpcb_workspace_bytes', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
+           'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram')
 
 
@@ -66,6 +66,7 @@ def load(path: str | None = None):
     lib.mpcb_abi_version.argtypes = []
     lib.mpcb_workspace_bytes.argtypes = [vp]
     lib.mpcb_workspace_bytes.restype = i64
+    lib.mpcb_path.argtypes = [vp]
     lib.mpcb_solve.argtypes = [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp]
     lib.mpcb_solve_iterate.argtypes = [vp, i64, vp, i64, vp, vp, vp, i64, vp, i64, vp, i64,
                                        vp, vp, vp, vp, vp]

@@ -57,6 +57,11 @@ class BatchedMPC:
     def workspace_bytes(self) -> int:
         return int(self.lib.mpcb_workspace_bytes(self._h))
 
+    @property
+    def path(self) -> str:
+        """'split' (nominal / Riccati / forward kernels) or 'fused' (one kernel)."""
+        return 'split' if self.lib.mpcb_path(self._h) == 1 else 'fused'
+
     def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):
         """Coerce to a contiguous device tensor of the handle dtype; return (tensor, stride)."""
         torch = _torch()

@@ -1,0 +1,63 @@
+"""``blasterModel``-compatible constructor (src/scripts/blastermodel.py:14-292).
+
+Same signature and call sequence as the reference:
+``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
+controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
+The weights / bounds given for the 17/6 reference model are sliced to the 12/4 rigid-body
+model this build implements (Q[:12,:12], R[:4,:4], thrust bounds controlBound[:, :4]).
+State bounds (statesBound) are accepted but not enforced (stage boxes are not part of the
+build; the reference scripts only pin x0).
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+
+from ..config import NU, NX, MPCConfig
+from .acados import AcadosOcpSolver, AcadosSimSolver
+
+
+class blasterModel:  # noqa: N801  (reference class name)
+    def __init__(self, mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
+                 controlBound, dtype: str = 'f64', batch: int = 1, device: int = 0):
+        self._M = float(mass)
+        self._J = np.asarray(J, dtype=np.float64)
+        self._arm_length_x = float(l_x)
+        self._arm_length_y = float(l_y)
+        self._c = float(c)
+        self._N = int(N)
+        self._Tf = float(Tf)
+        self._Q_weight = np.asarray(Q, dtype=np.float64)
+        self._Q_weight_t = np.asarray(Q_t, dtype=np.float64)
+        self._R_weight = np.asarray(R, dtype=np.float64)
+        self._blastThruster = float(blastThruster)
+        self._statesBound = np.asarray(statesBound, dtype=np.float64)
+        self._controlBound = np.asarray(controlBound, dtype=np.float64)
+        self._dtype, self._batch, self._device = dtype, int(batch), int(device)
+        self._cfg = None
+
+    def generateModel(self):
+        """Builds the problem definition (the dynamics themselves live in the HIP kernels)."""
+        cb = self._controlBound
+        self._cfg = MPCConfig(
+            N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
+            lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
+            Q=self._Q_weight[:NX, :NX], R=self._R_weight[:NU, :NU], QN=self._Q_weight_t[:NX, :NX],
+            lbu=cb[0][:NU], ubu=cb[1][:NU],
+            # default parameter vector of generateController (blastermodel.py:280-282) has
+            # T_blast = 2.2*9.81; the 12/4 quad configs use p[24] = 0 unless set(k,'p',...)
+            t_blast=0.0)
+        return 0
+
+    def generateController(self):
+        if self._cfg is None:
+            self.generateModel()
+        if self._statesBound.size and np.isfinite(self._statesBound).any():
+            warnings.warn('statesBound is not enforced by this build (stage state boxes are out of '
+                          'scope); x0 is pinned through set(0, "lbx"/"ubx")', stacklevel=2)
+        ocp = AcadosOcpSolver(self._cfg, batch=self._batch, device=self._device,
+                              json_file='acados_ocp_blasterModel.json')
+        sim = AcadosSimSolver(MPCConfig(**{**self._cfg.__dict__}), batch=self._batch,
+                              device=self._device)
+        return sim, ocp

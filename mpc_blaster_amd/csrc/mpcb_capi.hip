@@ -70,6 +70,7 @@ extern "C" const char* mpcb_last_error(void) { return g_err.c_str(); }
 extern "C" int mpcb_abi_version(void) { return MPCB_ABI_VERSION; }
 
 extern "C" int64_t mpcb_workspace_bytes(const mpcb_handle* h) { return h ? h->scratch_bytes : 0; }
+extern "C" int mpcb_path(const mpcb_handle* h) { return h ? h->split : -1; }
 
 template <class T>
 static void fill_weights(const mpcb_config& c, Weights<T>& w) {

@@ -14,7 +14,7 @@ import pytest
 
 from oracle.inputs import make_inputs
 from oracle.model import Params
-from oracle.ocp import OcpSpec, mpc_solve
+from oracle.ocp import OcpSpec, mpc_solve, stage_cost
 from oracle.rk4 import rk4_sens
 
 torch = pytest.importorskip('torch')
@@ -199,3 +199,68 @@ def test_full_size_c3_properties():
     o = mpc_solve(x0, xr, np.full((len(idx), N, 4), np.float32(22.0725), dtype=np.float64), _spec(N))
     assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-5
     assert relerr(X[idx].cpu().numpy(), o['X']).max() < 5e-5
+
+
+def test_closed_loop_matches_oracle_fp64():
+    """Receding-horizon loop (simulation_blaster.py:56-107) with the persistent SQP_RTI iterate."""
+    from mpc_blaster_amd.closed_loop import closed_loop
+    from oracle.rk4 import rk4_step
+    N, B, nsim = 10, 6, 12
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, 'f64', max_batch=B)
+    Xs, Us, st = closed_loop(m, inp['x0'], inp['xref'], inp['uref'], nsim)
+    torch.cuda.synchronize()
+    xbar = np.zeros((B, N + 1, 12))
+    ubar = np.zeros((B, N, 4))
+    x = inp['x0'].copy()
+    for i in range(nsim):
+        o = mpc_solve(x, inp['xref'], inp['uref'], _spec(N), mode='iterate', xbar=xbar, ubar=ubar)
+        xbar, ubar = o['X'], o['U']
+        assert relerr(Us[:, i].cpu().numpy(), o['u0']).max() < 1e-8
+        x = rk4_step(x, o['u0'], 1.0 / 30.0, Params())
+        assert relerr(Xs[:, i + 1].cpu().numpy(), x).max() < 1e-8
+    assert (st.cpu().numpy() == 0).all()
+
+
+def test_acados_facade_runs_reference_loop():
+    """simulation_blaster.py-style loop through the compat facade (12/4 slice of the reference
+    parameter set, reference-length 17/23 vectors sliced)."""
+    from mpc_blaster_amd.compat.blastermodel import blasterModel
+    J = np.diag([0.50781, 0.47314, 0.72975])
+    Q = np.zeros((17, 17))
+    np.fill_diagonal(Q, [1e3] * 6 + [5.0] * 3 + [10.0] * 3 + [1e-2] * 2 + [1e3] * 3)
+    R = np.zeros((6, 6))
+    np.fill_diagonal(R, [5e-2] * 4 + [1e-5] * 2)
+    cb = np.array([[0, 0, 0, 0, -0.0872665, -0.0872665], [65, 65, 65, 65, 0.0872665, 0.0872665]])
+    N = 15
+    b = blasterModel(9.0, J, 0.3434, 0.3475, N, N / 30.0, 0.03, Q, R, 10 * Q, 0.0,
+                     np.full((2, 17), np.nan), cb)
+    b.generateModel()
+    integrator, ocp_solver = b.generateController()
+    x = np.zeros(17)
+    yref = np.zeros(23)
+    yref[2] = 3.5
+    lbu, ubu = np.zeros(4), np.full(4, 65.0)
+    spec = OcpSpec(N=N, lbu=lbu, ubu=ubu)
+    xbar, ubar = np.zeros((1, N + 1, 12)), np.zeros((1, N, 4))
+    xs = x[:12].copy()
+    for i in range(5):
+        ocp_solver.set(0, 'lbx', x)
+        ocp_solver.set(0, 'ubx', x)
+        for k in range(N + 1):
+            ocp_solver.cost_set(k, 'yref', yref if k < N else yref[:17])
+        status = ocp_solver.solve()
+        u = ocp_solver.get(0, 'u')
+        o = mpc_solve(xs[None], np.broadcast_to(np.r_[0, 0, 3.5, [0] * 9], (1, N + 1, 12)),
+                      np.zeros((1, N, 4)), spec, mode='iterate', xbar=xbar, ubar=ubar)
+        xbar, ubar = o['X'], o['U']
+        assert status == 0
+        assert relerr(u[None], o['u0']).max() < 1e-8
+        assert abs(ocp_solver.get_cost() - float(stage_cost(o['X'], o['U'], np.broadcast_to(np.r_[0, 0, 3.5, [0] * 9], (1, N + 1, 12)), np.zeros((1, N, 4)), spec)[0])) < 1e-6 * max(1.0, ocp_solver.get_cost())
+        integrator.set('x', x)
+        integrator.set('u', np.r_[u, 0.0, 0.0])
+        assert integrator.solve() == 0
+        x = np.r_[integrator.get('x'), np.zeros(5)]
+        from oracle.rk4 import rk4_step
+        xs = rk4_step(xs[None], o['u0'], 1.0 / 30.0, Params())[0]
+        assert np.abs(x[:12] - xs).max() < 1e-9
