@@ -59,7 +59,8 @@ struct mpcb_handle {
   void* scratch;          // box path: per-slot workspace of the fused kernel
   int64_t slot_elems;
   int64_t scratch_bytes;
-  int split;              // 1: three-kernel split path; 0: fused single kernel
+  int split;              // 1: three-kernel split path; 0: one fused launch
+  int legacy;             // 1: small unconstrained batches use the single-pass kernel (A/B)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -134,11 +135,18 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   const size_t esz = f64 ? sizeof(double) : sizeof(float);
   // Path: the split kernels (thread-per-instance rollout/forward passes) need a large batch
   // to fill 1024 SIMDs; small batches and the input-box active-set loop use the fused kernel.
-  int64_t split_min = 16384;
+  int64_t split_min = 1;   // measured: the split kernels win at every batch size (c2: 4096)
   if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
   h->split = (!cfg->box_u && max_batch >= split_min) ? 1 : 0;
-  if (!h->split) {
+  h->legacy = 0;
+  if (const char* e = getenv("MPCB_FUSED_IMPL")) h->legacy = (strcmp(e, "v1") == 0) ? 1 : 0;
+  if (cfg->box_u || (!h->split && h->legacy)) {
+    // input boxes (and the v1 comparison path): the single-kernel solver of mpcb_solve.hip
     h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
+    h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
+  } else if (!h->split) {
+    // small unconstrained batches: nominal/Riccati/forward bodies fused in one launch
+    h->slot_elems = f64 ? fused_slot_elems<double>(cfg->N) : fused_slot_elems<float>(cfg->N);
     h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
   } else {
     // chunk of instances whose intermediates (~N*160 scalars each) stay near the 256 MiB
@@ -199,7 +207,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
                       const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
                       const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                       void* u0, void* X, void* U, int32_t* status, void* stream) {
-  if (h->split) {
+  if (!h->cfg.box_u && !(h->legacy && !h->split)) {
     SplitArgs<T> a;
     a.N = h->cfg.N;
     a.mode = mode;
@@ -215,6 +223,14 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
     a.fwd = (X || U || mode == MPCB_MODE_ITERATE) ? 1 : 0;
     const int N = h->cfg.N;
+    if (!h->split) {
+      a.XU = (T*)h->scratch;
+      const int64_t waves = (B + GROUPS - 1) / GROUPS;
+      const int grid = (int)(waves < h->grid ? waves : h->grid);
+      hipError_t e = launch_fused<T>(a, B, grid, (hipStream_t)stream);
+      if (e != hipSuccess) return fail(MPCB_E_HIP, "fused launch: %s", hipGetErrorString(e));
+      return MPCB_OK;
+    }
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       const int64_t nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
       T* base = (T*)h->scratch;

@@ -24,8 +24,46 @@ struct Model {
   T J[9], Jinv[9];
 };
 
-__device__ __forceinline__ void sc(double a, double* s, double* c) { sincos(a, s, c); }
-__device__ __forceinline__ void sc(float a, float* s, float* c) { sincosf(a, s, c); }
+// sin/cos for the attitude angles: Cody-Waite reduction by pi/2 + fdlibm / Cephes minimax
+// kernels (<= 1-2 ulp for |a| < 2^19).  The library sincos carries a Payne-Hanek large-argument
+// path that costs ~4x the instructions and registers on every call; here it is only the
+// (never taken in practice) fallback.  Three calls per f evaluation make this the dominant
+// cost of the nominal passes.
+__device__ __forceinline__ void sc(double a, double* s, double* c) {
+  if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
+  const double n = rint(a * 6.36619772367581382433e-01);           // 2/pi
+  double r = fma(-n, 1.57079632673412561417e+00, a);              // pio2_1 (33 bits)
+  r = fma(-n, 6.07710050650619224932e-11, r);                     // pio2_1t
+  const double z = r * r;
+  const double ps = -1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                    z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10))));
+  const double sr = fma(r * z, ps, r);
+  const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
+                    z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
+                    z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  const double cr = w + (((1.0 - w) - hz) + z * pc);
+  const int q = (int)n & 3;
+  const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+  *s = (q & 2) ? -s0 : s0;
+  *c = ((q + 1) & 2) ? -c0 : c0;
+}
+__device__ __forceinline__ void sc(float a, float* s, float* c) {
+  if (!(fabsf(a) < 8192.0f)) { sincosf(a, s, c); return; }
+  const float n = rintf(a * 0.636619772367581343f);
+  float r = fmaf(-n, 1.57079637050628662109375f, a);              // pio2 hi
+  r = fmaf(-n, -4.37113900018624283e-08f, r);                     // pio2 lo
+  const float z = r * r;
+  const float sr = fmaf(r * z, -1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f), r);
+  const float cr = fmaf(z * z, 4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f),
+                        fmaf(-0.5f, z, 1.0f));
+  const int q = (int)n & 3;
+  const float s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+  *s = (q & 2) ? -s0 : s0;
+  *c = ((q + 1) & 2) ? -c0 : c0;
+}
 
 // f and (optionally) its tangent.  wind may be nullptr-equivalent (w0=w1=w2=0).
 template <class T, bool TAN>
@@ -277,8 +315,11 @@ __device__ __forceinline__ void rk4_nom(const T* __restrict__ x, const T* __rest
 }
 
 // Tangent of the RK4 step along (dx, du) from the 4 captured stages at ``C`` (LIN_STAGE values).
-// ``cs`` is the element stride of C (1 for an AoS record, the chunk size for SoA layouts).
-template <class T>
+// ``cs`` is the element stride of C (1 for an AoS record, 4 for the quad-blocked SoA layout).
+// FENCE keeps each RK stage's scalars from being loaded up front (register diet when C is in
+// LDS next to a register-heavy Riccati body); without it all 80 loads issue together (one
+// memory round trip per interval instead of four, for latency-bound callers).
+template <class T, bool FENCE = true>
 __device__ __forceinline__ void rk4_tan(const T* __restrict__ C, const T* __restrict__ dx,
                                         const T* __restrict__ du, T h, const Model<T>& M,
                                         T* __restrict__ dxn, int64_t cs = 1) {
@@ -290,19 +331,19 @@ __device__ __forceinline__ void rk4_tan(const T* __restrict__ C, const T* __rest
   f_tan_lin<T>(c, dx, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
-  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+  if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
 #pragma unroll
   for (int i = 0; i < LIN_N; ++i) c[i] = C[(LIN_N + i) * cs];
   f_tan_lin<T>(c, dxs, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
-  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+  if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
 #pragma unroll
   for (int i = 0; i < LIN_N; ++i) c[i] = C[(2 * LIN_N + i) * cs];
   f_tan_lin<T>(c, dxs, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
-  asm volatile("" ::: "memory");  // load each stage's scalars just before use
+  if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
 #pragma unroll
   for (int i = 0; i < LIN_N; ++i) c[i] = C[(3 * LIN_N + i) * cs];
   f_tan_lin<T>(c, dxs, du, M, dk);

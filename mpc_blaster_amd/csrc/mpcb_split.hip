@@ -88,8 +88,7 @@ __device__ __forceinline__ T* soa(T* base, int k, int rec, int64_t nb, int64_t c
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) nominal_kernel(SplitArgs<T> a) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void nominal_body(const SplitArgs<T>& a, const int64_t c) {
   const int64_t nb = a.nb;
   if (c >= nb) return;
   const int64_t b = a.b0 + c;
@@ -137,7 +136,7 @@ __global__ void __launch_bounds__(256) nominal_kernel(SplitArgs<T> a) {
 }
 
 template <class T>
-__device__ __forceinline__ void riccati_body(const SplitArgs<T>& a) {
+__device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
   const int q = lane >> 4;
@@ -149,7 +148,6 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a) {
   const T s = a.s;
   const Weights<T>& W = *a.W;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
-  const int64_t c_raw = (int64_t)blockIdx.x * GROUPS + q;
   const bool valid = c_raw < a.nb;
   const int64_t c = valid ? c_raw : a.nb - 1;
   const int64_t b = a.b0 + c;
@@ -342,12 +340,14 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a) {
   }
 }
 
-template <class T>
-__global__ void __launch_bounds__(256) forward_kernel(SplitArgs<T> a) {
+// USE_CC: integrate the tangent from the captured linearisation scalars (fused small-batch
+// path: CC is slot-local and L2-resident) instead of re-evaluating f with sin/cos per stage
+// (split path: saves re-reading 80 scalars per stage from HBM).
+template <class T, bool USE_CC = false>
+__device__ __forceinline__ void forward_body(const SplitArgs<T>& a, const int64_t c) {
   // Recomputes the nominal RK4 stages (one fused value+tangent pass, mpcb_model.h rk4<T,true>)
   // instead of re-reading the 80 captured scalars: per stage it streams only xbar/ubar (16)
   // and the gains (52), prefetched one stage ahead.
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nb = a.nb;
   if (c >= nb) return;
   const int64_t b = a.b0 + c;
@@ -407,7 +407,16 @@ __global__ void __launch_bounds__(256) forward_kernel(SplitArgs<T> a) {
       if (k == 0) store_vec<NU>(a.u0 + b * NU, uo);
     }
     T phi[NX], dphi[NX];
-    rk4<T, true>(xb, dx, ub, du, a.h, a.M, w, phi, dphi);
+    if constexpr (USE_CC) {
+      rk4_tan<T, false>(soa(a.CC, k, CCS_REC, nb, c), dx, du, a.h, a.M, dphi, SS);
+      if (iterate) {
+        const T* gp = soa(a.GP, k, GP_REC, nb, c);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) phi[i] = gp[i * SS] + xn[i];
+      }
+    } else {
+      rk4<T, true>(xb, dx, ub, du, a.h, a.M, w, phi, dphi);
+    }
 #pragma unroll
     for (int i = 0; i < NX; ++i) dx[i] = iterate ? dphi[i] + (phi[i] - xn[i]) : dphi[i];
 #pragma unroll
@@ -431,11 +440,55 @@ template <class T> int64_t split_elems_per_instance(int N, int iterate) {
   return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR_REC + (iterate ? GP_REC : 0));
 }
 
+template <class T>
+__global__ void __launch_bounds__(256) nominal_kernel(SplitArgs<T> a) {
+  nominal_body<T>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+template <class T, bool USE_CC>
+__global__ void __launch_bounds__(256) forward_kernel(SplitArgs<T> a) {
+  forward_body<T, USE_CC>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_P2_WAVES_F32, 8)))
-riccati_kernel_f32(SplitArgs<float> a) { riccati_body<float>(a); }
+riccati_kernel_f32(SplitArgs<float> a) { riccati_body<float>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4)); }
 __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs<double> a) {
-  riccati_body<double>(a);
+  riccati_body<double>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+}
+
+// Small batches: the same three bodies run back to back inside ONE wavefront per 4 instances
+// (grid-stride over the batch), on a per-wavefront slot of the workspace.  A 4096-instance
+// batch is 1024 wavefronts = one per SIMD, so this launch is latency-bound either way; fusing
+// removes the two dependent launch boundaries and keeps the workspace L2-resident.
+template <class T>
+__global__ void __launch_bounds__(64) fused_kernel(SplitArgs<T> a, int64_t B, int64_t slot_elems) {
+  const int lane = threadIdx.x, q = lane >> 4, j = lane & 15;
+  T* slot = a.XU + (int64_t)blockIdx.x * slot_elems;
+  SplitArgs<T> s = a;
+  const int N = a.N;
+  s.XU = slot;
+  s.CC = s.XU + (int64_t)(N + 1) * GROUPS * XU_REC;
+  s.KR = s.CC + (int64_t)N * GROUPS * CCS_REC;
+  s.GP = s.KR + (int64_t)N * GROUPS * KR_REC;
+  for (int64_t wave = blockIdx.x; wave * GROUPS < B; wave += gridDim.x) {
+    s.b0 = wave * GROUPS;
+    s.nb = (B - s.b0 < GROUPS) ? B - s.b0 : GROUPS;
+    if (j == 0) nominal_body<T>(s, q);
+    __syncthreads();
+    riccati_body<T>(s, q);
+    __syncthreads();
+    if (s.fwd && j == 0) forward_body<T, true>(s, q);
+    __syncthreads();
+  }
+}
+
+template <class T> int64_t fused_slot_elems(int N) {
+  return split_elems_per_instance<T>(N, 1) * GROUPS;
+}
+
+template <class T>
+hipError_t launch_fused(const SplitArgs<T>& a, int64_t B, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((fused_kernel<T>), dim3(grid), dim3(64), 0, st, a, B, fused_slot_elems<T>(a.N));
+  return hipGetLastError();
 }
 
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st) {
@@ -446,10 +499,22 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     hipLaunchKernelGGL(riccati_kernel_f32, dim3(g64), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(riccati_kernel_f64, dim3(g64), dim3(64), 0, st, a);
-  if (a.fwd) hipLaunchKernelGGL((forward_kernel<T>), dim3(g256), dim3(256), 0, st, a);
+  // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
+  // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
+  // back from HBM.
+  if (a.fwd) {
+    if (a.nb <= 16384)
+      hipLaunchKernelGGL((forward_kernel<T, true>), dim3(g256), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((forward_kernel<T, false>), dim3(g256), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
+template hipError_t launch_fused<double>(const SplitArgs<double>&, int64_t, int, hipStream_t);
+template hipError_t launch_fused<float>(const SplitArgs<float>&, int64_t, int, hipStream_t);
+template int64_t fused_slot_elems<double>(int);
+template int64_t fused_slot_elems<float>(int);
 template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_split<float>(const SplitArgs<float>&, hipStream_t);
 template int64_t split_elems_per_instance<double>(int, int);
