@@ -28,6 +28,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 FLOP_PER_INTERVAL = 34785          # dense algorithmic flops per shooting interval
+# the Riccati kernel (dominant): RK4 sensitivities (21,996) minus the 4 f evaluations the nominal
+# pass already did (4 x 300), plus the Riccati backward recursion (12,309)
+FLOP_PER_INTERVAL_RICCATI = 21996 - 4 * 300 + 12309
 PEAK_TFLOPS = {'f64': 78.6, 'f32': 157.3}   # MI355X dense vector (= matrix) peaks, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 
@@ -90,12 +93,12 @@ def cpu_baseline(w, budget_s=12.0):
 
 
 def measured_traffic(workload: str):
-    """HBM bytes per launch from the committed PMC summary (tools/profile_pmc.sh), if present."""
+    """HBM bytes per Riccati launch from the committed PMC summary (tools/pmc_summary.py)."""
     p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
     if not os.path.exists(p):
         return None
     try:
-        return json.load(open(p)).get('hbm_bytes_per_solve_call')
+        return json.load(open(p)).get('hbm_bytes_per_riccati_launch')
     except Exception:
         return None
 
@@ -152,6 +155,15 @@ def run(w, world, rank, dev, steps, warmup):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     bad = int((outs[3] != 0).sum().item())
+    # per-phase device time (HIP events the library records on the launch stream around each
+    # kernel); a separate pass so that reading the events does not serialise the timed region
+    mpc.set_timing(True)
+    phases = []
+    for _ in range(steps):
+        step()
+        phases.append(mpc.last_timing())
+    mpc.set_timing(False)
+    phase_ms = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -159,19 +171,44 @@ def run(w, world, rank, dev, steps, warmup):
         bb = torch.tensor([bad], dtype=torch.int64, device=dev)
         dist.all_reduce(bb)
         bad = int(bb.item())
+        ph = torch.tensor([phase_ms[k] for k in sorted(phase_ms)], dtype=torch.float64, device=dev)
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+        phase_ms = dict(zip(sorted(phase_ms), ph.tolist()))
     path = 'split (3 kernels)' if mpc.path == 'split' else 'fused (1 kernel)'
     mpc.close()
-    return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path)
+    return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path, phase_ms=phase_ms,
+                split=path.startswith('split'))
 
 
 def summarize(w, r, world, steps):
     B, N = w['batch'], w['N']
     value = B * world * steps / r['elapsed']
-    flops_launch = FLOP_PER_INTERVAL * N * B
-    achieved_tf = flops_launch / (r['kern_ms'] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[w['dtype']]
+    ph = r['phase_ms']
+    per_interval = FLOP_PER_INTERVAL_RICCATI if r['split'] else FLOP_PER_INTERVAL
+    achieved_tf = per_interval * N * B / (ph['riccati'] * 1e-3) / 1e12
+    solve_tf = FLOP_PER_INTERVAL * N * B / (r['kern_ms'] * 1e-3) / 1e12
     hbm_gbs = compulsory_bytes(w) * B / (r['kern_ms'] * 1e-3) / 1e9
-    return value, achieved_tf, peak, hbm_gbs
+    roof = {'bound': 'mfma', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': achieved_tf / peak, 'traffic': measured_traffic(w['name']),
+            'kernel': 'riccati_kernel_%s' % w['dtype'] if r['split'] else 'solve (single launch)',
+            'kernel_ms': ph['riccati'],
+            'flop_per_launch': per_interval * N * B,
+            'phase_ms': ph,
+            'solve_ms': r['kern_ms'],
+            'solve_achieved': solve_tf,
+            'solve_frac': solve_tf / peak,
+            'hbm_compulsory_GBs': hbm_gbs,
+            'hbm_frac': hbm_gbs / HBM_PEAK_GBS,
+            'note': ('compute-bound path (SURVEY §8d: ~300-700 flop per compulsory byte). '
+                     f'Dominant kernel = Riccati pass: {per_interval} algorithmic flop per interval '
+                     '(dense count, §8d, minus the nominal f evaluations done by the rollout kernel) '
+                     'x N x B per launch, over its device time from HIP events on its launch stream. '
+                     f'solve_* = the whole solve ({FLOP_PER_INTERVAL} flop/interval) over all its '
+                     'kernels. peak = dense fp64/fp32 rate (gfx950 VALU and MFMA peaks are equal). '
+                     'traffic = HBM bytes per Riccati launch from PMC FETCH_SIZE x 2 + WRITE_SIZE '
+                     '(profiles/pmc_<workload>.json)')}
+    return value, roof
 
 
 def main():
@@ -207,17 +244,14 @@ def main():
     if world == 1 and not args.no_secondary and args.workload == 'c2':
         w3 = dict(WORKLOADS['c3'], name='c3')
         r3 = run(w3, 1, 0, dev, args.steps, args.warmup)
-        v3, a3, p3, h3 = summarize(w3, r3, 1, args.steps)
+        v3, roof3 = summarize(w3, r3, 1, args.steps)
+        roof3.pop('note')
         sec = {'workload': 'c3: batch 65536/GPU, N=20, fp32, sinusoidal refs (BASELINE configs[2])',
                'value': v3, 'unit': 'solves/s', 'ms_per_step': r3['elapsed'] / args.steps * 1e3,
-               'dtype': 'f32', 'path': r3['path'],
-               'roofline': {'bound': 'mfma', 'achieved': a3, 'peak': p3, 'unit': 'TFLOP/s', 'frac': a3 / p3,
-                            'traffic': measured_traffic('c3'), 'kernel_ms': r3['kern_ms'],
-                            'hbm_compulsory_GBs': h3},
-               'bad_status': r3['bad']}
+               'dtype': 'f32', 'path': r3['path'], 'roofline': roof3, 'bad_status': r3['bad']}
 
     if rank == 0:
-        value, achieved_tf, peak, hbm_gbs = summarize(w, r, world, args.steps)
+        value, roof = summarize(w, r, world, args.steps)
         B, N = w['batch'], w['N']
         line = {
             'metric': 'MPC solves/sec (N=%d, nx=12, nu=4)' % N,
@@ -239,15 +273,7 @@ def main():
                        'parallelism': f'instance-sharded x{world}'
                                       + ((' + RCCL all_reduce(histogram)' if w['hist'] else ' + RCCL all_gather(u0)')
                                          if world > 1 else '')},
-            'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': achieved_tf / peak, 'traffic': measured_traffic(w['name']),
-                         'note': (f'compute-bound path (SURVEY §8d: ~300-700 flop per compulsory byte); '
-                                  f'algorithmic flops = {FLOP_PER_INTERVAL} x N x B per solve launch '
-                                  '(dense count) over the device time of the solve launch(es), '
-                                  'HIP events on the launch stream; peak = dense fp64/fp32 rate '
-                                  '(gfx950 VALU and MFMA peaks are equal)'),
-                         'kernel_ms': r['kern_ms'], 'hbm_compulsory_GBs': hbm_gbs,
-                         'hbm_frac': hbm_gbs / HBM_PEAK_GBS},
+            'roofline': roof,
             'bad_status': r['bad'],
         }
         if sec is not None:

@@ -82,6 +82,13 @@ int64_t mpcb_workspace_bytes(const mpcb_handle* h);
 /* Kernel path chosen at creation: 0 = fused single kernel (small batches, input boxes),
  * 1 = split nominal / Riccati / forward kernels (large unconstrained batches). */
 int mpcb_path(const mpcb_handle* h);
+/* Optional device timing of later solves: HIP events recorded on the launch stream around each
+ * kernel phase.  ``mpcb_last_timing`` waits for the last timed solve and writes the device
+ * milliseconds of its phases: ms[0] nominal rollout, ms[1] Riccati (the dominant kernel; the
+ * single launch on the fused / box paths), ms[2] forward pass.  Summed over chunks (up to 64).
+ * No reference counterpart (acados' ``get_stats('time_tot')`` is host wall time). */
+int mpcb_set_timing(mpcb_handle* h, int enable);
+int mpcb_last_timing(mpcb_handle* h, float ms[3]);
 
 /*
  * One SQP_RTI step for B independent instances, linearised at the RK4 rollout of u_ref from

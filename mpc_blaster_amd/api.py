@@ -62,6 +62,16 @@ class BatchedMPC:
         """'split' (nominal / Riccati / forward kernels) or 'fused' (one kernel)."""
         return 'split' if self.lib.mpcb_path(self._h) == 1 else 'fused'
 
+    def set_timing(self, enable: bool = True):
+        """Record HIP events around each kernel phase of later solves (see ``last_timing``)."""
+        _lib.check(self.lib.mpcb_set_timing(self._h, 1 if enable else 0))
+
+    def last_timing(self) -> dict:
+        """Device ms of the last timed solve's phases: nominal, riccati (dominant), forward."""
+        ms = (ctypes.c_float * 3)()
+        _lib.check(self.lib.mpcb_last_timing(self._h, ms))
+        return dict(nominal=ms[0], riccati=ms[1], forward=ms[2])
+
     def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):
         """Coerce to a contiguous device tensor of the handle dtype; return (tensor, stride)."""
         torch = _torch()

@@ -65,6 +65,13 @@ struct mpcb_handle {
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
   Model<float> Mf;
+  // optional per-phase device timing (mpcb_set_timing): 4 events per split chunk, or ev[0][0..1]
+  // around the single launch of the fused / box paths
+  static constexpr int TCHUNKS = 64;
+  int timing = 0;
+  int timed_chunks = 0;   // chunks recorded by the last solve (0: nothing recorded)
+  int timed_split = 0;
+  hipEvent_t ev[TCHUNKS][4] = {};
 };
 
 extern "C" const char* mpcb_last_error(void) { return g_err.c_str(); }
@@ -196,6 +203,9 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
 extern "C" int mpcb_destroy(mpcb_handle* h) {
   if (!h) return MPCB_OK;
   (void)hipSetDevice(h->device);
+  for (auto& c : h->ev)
+    for (auto& e : c)
+      if (e) (void)hipEventDestroy(e);
   (void)hipFree(h->scratch);
   (void)hipFree(h->weights);
   delete h;
@@ -227,10 +237,17 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.XU = (T*)h->scratch;
       const int64_t waves = (B + GROUPS - 1) / GROUPS;
       const int grid = (int)(waves < h->grid ? waves : h->grid);
+      if (h->timing) (void)hipEventRecord(h->ev[0][0], (hipStream_t)stream);
       hipError_t e = launch_fused<T>(a, B, grid, (hipStream_t)stream);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "fused launch: %s", hipGetErrorString(e));
+      if (h->timing) {
+        (void)hipEventRecord(h->ev[0][1], (hipStream_t)stream);
+        h->timed_chunks = 1;
+        h->timed_split = 0;
+      }
       return MPCB_OK;
     }
+    int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       const int64_t nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
       T* base = (T*)h->scratch;
@@ -241,8 +258,14 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.CC = a.XU + (int64_t)(N + 1) * nbp * XU_REC;
       a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
       a.GP = a.KR + (int64_t)N * nbp * KR_REC;
-      hipError_t e = launch_split<T>(a, (hipStream_t)stream);
+      hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
+      hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));
+      ++chunk_i;
+    }
+    if (h->timing) {
+      h->timed_chunks = chunk_i < mpcb_handle::TCHUNKS ? chunk_i : mpcb_handle::TCHUNKS;
+      h->timed_split = 1;
     }
     return MPCB_OK;
   }
@@ -266,8 +289,45 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
   a.slot_elems = h->slot_elems;
   const int64_t waves = (B + GROUPS - 1) / GROUPS;
   const int grid = (int)(waves < h->grid ? waves : h->grid);
+  if (h->timing) (void)hipEventRecord(h->ev[0][0], (hipStream_t)stream);
   hipError_t e = launch_solve<T>(a, grid, (hipStream_t)stream);
   if (e != hipSuccess) return fail(MPCB_E_HIP, "solve launch: %s", hipGetErrorString(e));
+  if (h->timing) {
+    (void)hipEventRecord(h->ev[0][1], (hipStream_t)stream);
+    h->timed_chunks = 1;
+    h->timed_split = 0;
+  }
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_set_timing(mpcb_handle* h, int enable) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (enable && !h->ev[0][0]) {
+    hipError_t e = hipSetDevice(h->device);
+    for (auto& c : h->ev)
+      for (auto& ev : c)
+        if (e == hipSuccess) e = hipEventCreate(&ev);
+    if (e != hipSuccess) return fail(MPCB_E_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+  }
+  h->timing = enable ? 1 : 0;
+  h->timed_chunks = 0;
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_last_timing(mpcb_handle* h, float* ms) {
+  if (!h || !ms) return fail(MPCB_E_INVALID, "null argument");
+  ms[0] = ms[1] = ms[2] = 0.f;
+  if (!h->timing || h->timed_chunks == 0) return fail(MPCB_E_INVALID, "no timed solve recorded");
+  for (int c = 0; c < h->timed_chunks; ++c) {
+    const int phases = h->timed_split ? 3 : 1;
+    for (int p = 0; p < phases; ++p) {
+      float t = 0.f;
+      hipError_t e = hipEventSynchronize(h->ev[c][p + 1]);
+      if (e == hipSuccess) e = hipEventElapsedTime(&t, h->ev[c][p], h->ev[c][p + 1]);
+      if (e != hipSuccess) return fail(MPCB_E_HIP, "event timing: %s", hipGetErrorString(e));
+      ms[h->timed_split ? p : 1] += t;
+    }
+  }
   return MPCB_OK;
 }
 

@@ -75,7 +75,9 @@ struct SplitArgs {
   T* XU; T* CC; T* GP; T* KR;
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
 };
-template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st);
+// ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
+template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
+                                           hipEvent_t* ev = nullptr);
 // small batches: one fused launch, one wavefront per 4 instances, slot-local workspace
 template <class T> hipError_t launch_fused(const SplitArgs<T>& a, int64_t B, int grid, hipStream_t st);
 template <class T> int64_t fused_slot_elems(int N);

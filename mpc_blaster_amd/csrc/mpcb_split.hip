@@ -491,14 +491,17 @@ hipError_t launch_fused(const SplitArgs<T>& a, int64_t B, int grid, hipStream_t 
   return hipGetLastError();
 }
 
-template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st) {
+template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
   const unsigned g256 = (unsigned)((a.nb + 255) / 256);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL((nominal_kernel<T>), dim3(g256), dim3(256), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[1], st);
   if constexpr (sizeof(T) == 4)
     hipLaunchKernelGGL(riccati_kernel_f32, dim3(g64), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(riccati_kernel_f64, dim3(g64), dim3(64), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[2], st);
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
@@ -508,6 +511,7 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     else
       hipLaunchKernelGGL((forward_kernel<T, false>), dim3(g256), dim3(256), 0, st, a);
   }
+  if (ev) (void)hipEventRecord(ev[3], st);
   return hipGetLastError();
 }
 
@@ -515,8 +519,8 @@ template hipError_t launch_fused<double>(const SplitArgs<double>&, int64_t, int,
 template hipError_t launch_fused<float>(const SplitArgs<float>&, int64_t, int, hipStream_t);
 template int64_t fused_slot_elems<double>(int);
 template int64_t fused_slot_elems<float>(int);
-template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t);
-template hipError_t launch_split<float>(const SplitArgs<float>&, hipStream_t);
+template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t, hipEvent_t*);
+template hipError_t launch_split<float>(const SplitArgs<float>&, hipStream_t, hipEvent_t*);
 template int64_t split_elems_per_instance<double>(int, int);
 template int64_t split_elems_per_instance<float>(int, int);
 

@@ -175,6 +175,25 @@ def test_u0_only_path_equals_full_path(path):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('path,box', [('fused', False), ('split', False), (None, True)])
+def test_phase_timing_events(path, box):
+    """mpcb_set_timing / mpcb_last_timing: per-phase device ms, and timing changes no result."""
+    N, B = 20, 256
+    inp = make_inputs('c3', ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, 'f32', box=box, max_batch=B, path=path)
+    a = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=False).clone()
+    m.set_timing(True)
+    b = m.solve(inp['x0'], inp['xref'], inp['uref'], want_traj=False)
+    t = m.last_timing()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert t['riccati'] > 0
+    if m.path == 'split':
+        assert t['nominal'] > 0 and t['forward'] < t['riccati']   # u0 only: no forward kernel
+    else:
+        assert t['nominal'] == 0 and t['forward'] == 0
+
+
 def test_full_size_c3_properties():
     """BASELINE c3 at full size: statuses, finiteness, shard invariance, sampled oracle parity."""
     from mpc_blaster_amd import BatchedMPC, MPCConfig
