@@ -79,3 +79,19 @@ def test_config_validation():
     cc = c.to_c()
     assert cc.box_u == 1 and cc.N == 30 and abs(cc.cost_scale - 1 / 30) < 1e-15
     assert list(cc.ubu)[:4] == [65.0] * 4
+
+
+def test_config_defaults_equal_reference_json_slice():
+    """MPCConfig defaults = the 12/4 slice of acados_ocp_blasterModel.json (fixture)."""
+    import json
+    import os
+    from mpc_blaster_amd import MPCConfig
+    pin = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'ocp_json_pin.json')))
+    c = MPCConfig()
+    W = np.asarray(pin['W'])
+    assert np.array_equal(c.Q, W[:12, :12])
+    assert np.array_equal(c.R, W[17:21, 17:21])
+    assert np.array_equal(c.QN, np.asarray(pin['W_e'])[:12, :12])
+    assert abs(c.dt - pin['solver_options']['time_steps'][0]) < 1e-15
+    b = MPCConfig(lbu=np.asarray(pin['lbu'][:4]), ubu=np.asarray(pin['ubu'][:4]))
+    assert b.to_c().box_u == 1
