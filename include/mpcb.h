@@ -79,8 +79,8 @@ const char* mpcb_last_error(void);
 int mpcb_abi_version(void);
 /* Workspace bytes owned by the handle (informational). */
 int64_t mpcb_workspace_bytes(const mpcb_handle* h);
-/* Kernel path chosen at creation: 0 = fused single kernel (small batches, input boxes),
- * 1 = split nominal / Riccati / forward kernels (large unconstrained batches). */
+/* Kernel path chosen at creation: 1 = split nominal / Riccati / forward kernels (unconstrained),
+ * 0 = single-kernel solver (input boxes; small batches when MPCB_SPLIT_MIN_BATCH asks for it). */
 int mpcb_path(const mpcb_handle* h);
 /* Optional device timing of later solves: HIP events recorded on the launch stream around each
  * kernel phase.  ``mpcb_last_timing`` waits for the last timed solve and writes the device
@@ -101,7 +101,7 @@ int mpcb_last_timing(mpcb_handle* h, float ms[3]);
  *   wind  [B|1, 3] or NULL   world-frame disturbance force (build extension, c5)
  *   u0    [B, nu]            first-step control u0* (required)
  *   X     [B, N+1, nx]|NULL  predicted state trajectory xbar + dx (linear prediction)
- *   U     [B, N, nu]|NULL    predicted controls
+ *   U     [B, N, nu]|NULL    predicted controls (X and U 16-byte aligned)
  *   status[B] int32          per-instance status
  */
 int mpcb_solve(mpcb_handle* h, int64_t B,

@@ -56,17 +56,16 @@ struct mpcb_handle {
   int64_t max_batch;
   int grid;              // resident slots (one wavefront of GROUPS instances each)
   void* weights;         // Weights<T>
-  void* scratch;          // box path: per-slot workspace of the fused kernel
+  void* scratch;          // split: chunk workspace; single-kernel solver: per-slot workspace
   int64_t slot_elems;
   int64_t scratch_bytes;
-  int split;              // 1: three-kernel split path; 0: one fused launch
-  int legacy;             // 1: small unconstrained batches use the single-pass kernel (A/B)
+  int split;              // 1: three-kernel split path; 0: single-kernel solver (boxes)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
   Model<float> Mf;
   // optional per-phase device timing (mpcb_set_timing): 4 events per split chunk, or ev[0][0..1]
-  // around the single launch of the fused / box paths
+  // around the single launch of the single-kernel solver
   static constexpr int TCHUNKS = 64;
   int timing = 0;
   int timed_chunks = 0;   // chunks recorded by the last solve (0: nothing recorded)
@@ -140,20 +139,14 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   if (grid > waves_needed) grid = waves_needed;
   h->grid = (int)grid;
   const size_t esz = f64 ? sizeof(double) : sizeof(float);
-  // Path: the split kernels (thread-per-instance rollout/forward passes) need a large batch
-  // to fill 1024 SIMDs; small batches and the input-box active-set loop use the fused kernel.
-  int64_t split_min = 1;   // measured: the split kernels win at every batch size (c2: 4096)
+  // Path: the split kernels win at every measured batch size (c2: 4096); the single-kernel
+  // solver (mpcb_solve.hip) serves the input-box active-set loop and, on request
+  // (MPCB_SPLIT_MIN_BATCH above the batch), small unconstrained batches.
+  int64_t split_min = 1;
   if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
   h->split = (!cfg->box_u && max_batch >= split_min) ? 1 : 0;
-  h->legacy = 0;
-  if (const char* e = getenv("MPCB_FUSED_IMPL")) h->legacy = (strcmp(e, "v1") == 0) ? 1 : 0;
-  if (cfg->box_u || (!h->split && h->legacy)) {
-    // input boxes (and the v1 comparison path): the single-kernel solver of mpcb_solve.hip
+  if (!h->split) {
     h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
-    h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
-  } else if (!h->split) {
-    // small unconstrained batches: nominal/Riccati/forward bodies fused in one launch
-    h->slot_elems = f64 ? fused_slot_elems<double>(cfg->N) : fused_slot_elems<float>(cfg->N);
     h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
   } else {
     // chunk of instances whose intermediates (~N*160 scalars each) stay near the 256 MiB
@@ -217,7 +210,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
                       const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
                       const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                       void* u0, void* X, void* U, int32_t* status, void* stream) {
-  if (!h->cfg.box_u && !(h->legacy && !h->split)) {
+  if (h->split) {
     SplitArgs<T> a;
     a.N = h->cfg.N;
     a.mode = mode;
@@ -233,20 +226,6 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
     a.fwd = (X || U || mode == MPCB_MODE_ITERATE) ? 1 : 0;
     const int N = h->cfg.N;
-    if (!h->split) {
-      a.XU = (T*)h->scratch;
-      const int64_t waves = (B + GROUPS - 1) / GROUPS;
-      const int grid = (int)(waves < h->grid ? waves : h->grid);
-      if (h->timing) (void)hipEventRecord(h->ev[0][0], (hipStream_t)stream);
-      hipError_t e = launch_fused<T>(a, B, grid, (hipStream_t)stream);
-      if (e != hipSuccess) return fail(MPCB_E_HIP, "fused launch: %s", hipGetErrorString(e));
-      if (h->timing) {
-        (void)hipEventRecord(h->ev[0][1], (hipStream_t)stream);
-        h->timed_chunks = 1;
-        h->timed_split = 0;
-      }
-      return MPCB_OK;
-    }
     int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       const int64_t nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
@@ -332,19 +311,22 @@ extern "C" int mpcb_last_timing(mpcb_handle* h, float* ms) {
 }
 
 static int check_solve(mpcb_handle* h, int64_t B, const void* x0, const void* xref, const void* uref,
-                       const void* u0, const int32_t* status) {
+                       const void* u0, const void* X, const void* U, const int32_t* status) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
   if (B < 0 || B > h->max_batch)
     return fail(MPCB_E_INVALID, "batch %lld exceeds max_batch %lld", (long long)B, (long long)h->max_batch);
   if (B > 0 && (!x0 || !xref || !uref || !u0 || !status))
     return fail(MPCB_E_INVALID, "x0, xref, uref, u0 and status are required");
+  // the trajectory outputs are written in 16-byte chunks
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(U)) & 15)
+    return fail(MPCB_E_INVALID, "X and U must be 16-byte aligned");
   return MPCB_OK;
 }
 
 extern "C" int mpcb_solve(mpcb_handle* h, int64_t B, const void* x0, int64_t x0_sb, const void* xref,
                int64_t xref_sb, const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                void* u0, void* X, void* U, int32_t* status, void* stream) {
-  int rc = check_solve(h, B, x0, xref, uref, u0, status);
+  int rc = check_solve(h, B, x0, xref, uref, u0, X, U, status);
   if (rc || B == 0) return rc;
   HIP_TRY(hipSetDevice(h->device));
   if (h->cfg.dtype == MPCB_F64)
@@ -358,7 +340,7 @@ extern "C" int mpcb_solve_iterate(mpcb_handle* h, int64_t B, const void* x0, int
                        const void* ubar, const void* xref, int64_t xref_sb, const void* uref,
                        int64_t uref_sb, const void* wind, int64_t wind_sb, void* u0, void* X, void* U,
                        int32_t* status, void* stream) {
-  int rc = check_solve(h, B, x0, xref, uref, u0, status);
+  int rc = check_solve(h, B, x0, xref, uref, u0, X, U, status);
   if (rc || B == 0) return rc;
   if (!xbar || !ubar) return fail(MPCB_E_INVALID, "xbar and ubar are required");
   HIP_TRY(hipSetDevice(h->device));

@@ -78,9 +78,6 @@ struct SplitArgs {
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
                                            hipEvent_t* ev = nullptr);
-// small batches: one fused launch, one wavefront per 4 instances, slot-local workspace
-template <class T> hipError_t launch_fused(const SplitArgs<T>& a, int64_t B, int grid, hipStream_t st);
-template <class T> int64_t fused_slot_elems(int N);
 template <class T> int64_t split_elems_per_instance(int N, int iterate);  // per 64-padded instance
 template <class T> int64_t solve_slot_elems(int N, int box);
 

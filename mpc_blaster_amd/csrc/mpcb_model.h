@@ -314,41 +314,48 @@ __device__ __forceinline__ void rk4_nom(const T* __restrict__ x, const T* __rest
   for (int i = 0; i < NX; ++i) xn[i] = x[i] + h6 * (xn[i] + k[i]);
 }
 
-// Tangent of the RK4 step along (dx, du) from the 4 captured stages at ``C`` (LIN_STAGE values).
-// ``cs`` is the element stride of C (1 for an AoS record, 4 for the quad-blocked SoA layout).
-// FENCE keeps each RK stage's scalars from being loaded up front (register diet when C is in
-// LDS next to a register-heavy Riccati body); without it all 80 loads issue together (one
-// memory round trip per interval instead of four, for latency-bound callers).
-template <class T, bool FENCE = true>
-__device__ __forceinline__ void rk4_tan(const T* __restrict__ C, const T* __restrict__ dx,
-                                        const T* __restrict__ du, T h, const Model<T>& M,
-                                        T* __restrict__ dxn, int64_t cs = 1) {
+// Tangent of the RK4 step along (dx, du) from the 4 captured stages (LIN_STAGE values; ``get(i)``
+// returns captured scalar i).  FENCE keeps each RK stage's scalars from being loaded up front
+// (register diet when they sit in LDS next to a register-heavy Riccati body); without it all 80
+// loads issue together (one memory round trip per interval, for latency-bound callers).
+template <class T, bool FENCE = true, class Get>
+__device__ __forceinline__ void rk4_tan_g(Get get, const T* __restrict__ dx,
+                                          const T* __restrict__ du, T h, const Model<T>& M,
+                                          T* __restrict__ dxn) {
   constexpr int NX = 12;
   T dk[NX], dxs[NX], c[LIN_N];
   const T h2 = T(0.5) * h, h6 = h / T(6);
 #pragma unroll
-  for (int i = 0; i < LIN_N; ++i) c[i] = C[(i) * cs];
+  for (int i = 0; i < LIN_N; ++i) c[i] = get(i);
   f_tan_lin<T>(c, dx, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
   if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
 #pragma unroll
-  for (int i = 0; i < LIN_N; ++i) c[i] = C[(LIN_N + i) * cs];
+  for (int i = 0; i < LIN_N; ++i) c[i] = get(LIN_N + i);
   f_tan_lin<T>(c, dxs, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
-  if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
+  if constexpr (FENCE) asm volatile("" ::: "memory");
 #pragma unroll
-  for (int i = 0; i < LIN_N; ++i) c[i] = C[(2 * LIN_N + i) * cs];
+  for (int i = 0; i < LIN_N; ++i) c[i] = get(2 * LIN_N + i);
   f_tan_lin<T>(c, dxs, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
-  if constexpr (FENCE) asm volatile("" ::: "memory");  // load each stage's scalars just before use
+  if constexpr (FENCE) asm volatile("" ::: "memory");
 #pragma unroll
-  for (int i = 0; i < LIN_N; ++i) c[i] = C[(3 * LIN_N + i) * cs];
+  for (int i = 0; i < LIN_N; ++i) c[i] = get(3 * LIN_N + i);
   f_tan_lin<T>(c, dxs, du, M, dk);
 #pragma unroll
   for (int i = 0; i < NX; ++i) dxn[i] = dx[i] + h6 * (dxn[i] + dk[i]);
+}
+
+// The same from a strided record ``C`` (``cs`` = element stride: 1 for AoS, 4 for quad-blocked).
+template <class T, bool FENCE = true>
+__device__ __forceinline__ void rk4_tan(const T* __restrict__ C, const T* __restrict__ dx,
+                                        const T* __restrict__ du, T h, const Model<T>& M,
+                                        T* __restrict__ dxn, int64_t cs = 1) {
+  rk4_tan_g<T, FENCE>([&](int i) { return C[i * cs]; }, dx, du, h, M, dxn);
 }
 
 }  // namespace mpcb

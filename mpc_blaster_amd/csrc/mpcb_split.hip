@@ -15,6 +15,8 @@
 // Intermediates live in a chunk workspace sized to stay in the 256 MiB Infinity Cache.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/mpcb.h"
 #include "mpcb_common.h"
 
@@ -87,10 +89,104 @@ __device__ __forceinline__ T* soa(T* base, int k, int rec, int64_t nb, int64_t c
   return base + (((int64_t)k * nq + (c >> 2)) * rec) * SS + (c & (SS - 1));
 }
 
+// ---- wave-staged workspace / output traffic of the thread-per-instance passes (P1, P3) ------
+// P1 and P3 run one thread per instance in single-wave workgroups: 64 instances = 16 quads.  For
+// a fixed stage k the wave's records of any quad-blocked array are ONE contiguous run of
+// 16 x REC x 4 elements, but element-per-thread accesses touch 16 cache lines per instruction
+// (measured: the CC stores were 2/3 of P1's time at c3, the CC loads 1/3 of P3's at c2, the
+// X/U stores another 1/3 of P3's).  So stores are staged in LDS and written as 16-B chunks
+// (P1: 1 KiB of contiguous workspace per wave-instruction), and loads arrive by LDS-DMA
+// (global_load_lds_dwordx4) one stage ahead into an element-major [REC][64] image that each
+// thread reads conflict-free at img[i * 64 + lane].
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int WAVE = 64, WQ = WAVE / SS;
+
+template <class T> __device__ __forceinline__ void copy16(T* dst, const T* src) {
+  *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+}
+
+// Chunks t = lane, lane + 64, ... < 64 * NI of an LDS -> global copy, LDS reads issued in batches
+// of 8 ahead of their stores so the LDS latency is paid once per batch, not once per chunk.
+template <int NI, class Src, class Dst>
+__device__ __forceinline__ void copy_chunks(int lane, Src src, Dst dst) {
+#pragma unroll
+  for (int g = 0; g < NI; g += 8) {
+    u32x4 r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (g + e < NI) r[e] = *reinterpret_cast<const u32x4*>(src((g + e) * 64 + lane));
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (g + e < NI) *reinterpret_cast<u32x4*>(dst((g + e) * 64 + lane)) = r[e];
+  }
+}
+
+// LDS staging of the wave's 16 quad records of a REC-element stage record; the quad stride
+// REC*4+4 keeps the per-thread writes bank-conflict free (fp32 and fp64).
+template <class T, int REC>
+struct QuadStore {
+  static constexpr int STRIDE = REC * SS + 4;
+  static constexpr int ELEMS = WQ * STRIDE;
+  T* buf;
+  __device__ __forceinline__ void put(int lane, int i, T v) const {
+    buf[(lane >> 2) * STRIDE + i * SS + (lane & 3)] = v;
+  }
+  // dst = the wave's first quad record (soa(base, k, REC, nb, c0)); nqv quads are valid.  The
+  // wave's records are contiguous in the workspace, so chunk t goes to dst + t * V.
+  __device__ __forceinline__ void flush(int lane, T* dst, int nqv) const {
+    constexpr int V = 16 / sizeof(T), CPQ = REC * SS / V, TOT = WQ * CPQ;
+    static_assert(TOT % WAVE == 0, "whole wave-instructions");
+    auto src = [&](int t) { return buf + t * V + (t / CPQ) * 4; };
+    if (nqv == WQ) {
+      copy_chunks<TOT / WAVE>(lane, src, [&](int t) { return dst + t * V; });
+    } else {
+      for (int t = lane; t < nqv * CPQ; t += WAVE) copy16(dst + t * V, src(t));
+    }
+  }
+};
+
+// LDS-DMA of the wave's stage record (REC elements per instance) into img[i * 64 + lane].
+// Chunk t of the wave-linear DMA image holds element i = t / CPI of the V = 16/sizeof(T)
+// consecutive instances (t % CPI) * V ..; lane l of instruction m therefore always reads the same
+// quad column at row i = m * IPI + l / CPI, i.e. src_lane + m * IPI * 4 (``dma_lane_offset``).
+typedef __attribute__((address_space(3))) void lds_void;
+template <class T> struct Dma {
+  static constexpr int V = 16 / sizeof(T), CPI = WAVE / V, IPI = WAVE / CPI;
+  // element offset of lane l's first chunk inside a wave's record run; REC = record length
+  __device__ static __forceinline__ int lane_offset(int lane, int rec) {
+    const int part = lane % CPI;
+    return ((part * V) / SS * rec + lane / CPI) * SS + (part * V) % SS;
+  }
+  __device__ static __forceinline__ bool lane_valid(int lane, int nqv) { return (lane % CPI) * V / SS < nqv; }
+};
+template <class T, int REC>
+__device__ __forceinline__ void dma_record(unsigned img, const T* src_lane) {
+  using D = Dma<T>;
+  static_assert((REC * D::CPI) % WAVE == 0, "record must fill whole wave-instructions");
+#pragma unroll
+  for (int m = 0; m < REC * D::CPI / WAVE; ++m)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src_lane + m * D::IPI * SS),
+        (lds_void*)(size_t)(img + m * WAVE * 16), 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <class T>
-__device__ __forceinline__ void nominal_body(const SplitArgs<T>& a, const int64_t c) {
+__device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
+  __shared__ __attribute__((aligned(16))) T lds_cc[QuadStore<T, CCS_REC>::ELEMS];
+  __shared__ __attribute__((aligned(16))) T lds_xu[QuadStore<T, XU_REC>::ELEMS];
+  __shared__ __attribute__((aligned(16))) T lds_gp[QuadStore<T, GP_REC>::ELEMS];
+  const QuadStore<T, CCS_REC> ccs{lds_cc};
+  const QuadStore<T, XU_REC> xus{lds_xu};
+  const QuadStore<T, GP_REC> gps{lds_gp};
+  const int lane = threadIdx.x;
   const int64_t nb = a.nb;
-  if (c >= nb) return;
+  const int64_t c0 = (int64_t)blockIdx.x * WAVE;
+  // tail lanes recompute the chunk's last instance; their slots are quad padding or unflushed
+  const int64_t c = (c0 + lane < nb) ? c0 + lane : nb - 1;
+  const int64_t nq = (nb + SS - 1) / SS;
+  const int nqv = (int)((nq - c0 / SS) < WQ ? nq - c0 / SS : WQ);
   const int64_t b = a.b0 + c;
   const int N = a.N;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
@@ -106,33 +202,35 @@ __device__ __forceinline__ void nominal_body(const SplitArgs<T>& a, const int64_
   for (int k = 0; k < N; ++k) {
     if (iterate) load_vec<NX>(xbp + (int64_t)k * NX, x);
     load_vec<NU>(iterate ? ubp + (int64_t)k * NU : ur + (int64_t)k * NU, u);
-    T* xu = soa(a.XU, k, XU_REC, nb, c);
 #pragma unroll
-    for (int i = 0; i < NX; ++i) xu[i * SS] = x[i];
+    for (int i = 0; i < NX; ++i) xus.put(lane, i, x[i]);
 #pragma unroll
-    for (int m = 0; m < NU; ++m) xu[(NX + m) * SS] = u[m];
-    T* cc = soa(a.CC, k, CCS_REC, nb, c);
+    for (int m = 0; m < NU; ++m) xus.put(lane, NX + m, u[m]);
     T xn[NX];
     rk4_nom<T>(x, u, a.h, a.M, w, xn, [&](int stage, const T* cv) {
 #pragma unroll
-      for (int i = 0; i < LIN_N; ++i) cc[(stage * LIN_N + i) * SS] = cv[i];
+      for (int i = 0; i < LIN_N; ++i) ccs.put(lane, stage * LIN_N + i, cv[i]);
     });
     if (iterate) {
       const T* nx = xbp + (int64_t)(k + 1) * NX;
-      T* gp = soa(a.GP, k, GP_REC, nb, c);
 #pragma unroll
-      for (int i = 0; i < NX; ++i) gp[i * SS] = xn[i] - nx[i];
+      for (int i = 0; i < NX; ++i) gps.put(lane, i, xn[i] - nx[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < NX; ++i) x[i] = xn[i];
     }
+    // one wave per workgroup: its LDS operations complete in order, so no barrier (which would
+    // also drain the stores) is needed between the per-thread puts and the chunked flush
+    xus.flush(lane, soa(a.XU, k, XU_REC, nb, c0), nqv);
+    ccs.flush(lane, soa(a.CC, k, CCS_REC, nb, c0), nqv);
+    if (iterate) gps.flush(lane, soa(a.GP, k, GP_REC, nb, c0), nqv);
   }
   if (iterate) load_vec<NX>(xbp + (int64_t)N * NX, x);
-  T* xu = soa(a.XU, N, XU_REC, nb, c);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) xu[i * SS] = x[i];
+  for (int i = 0; i < NX; ++i) xus.put(lane, i, x[i]);
 #pragma unroll
-  for (int m = 0; m < NU; ++m) xu[(NX + m) * SS] = T(0);
+  for (int m = 0; m < NU; ++m) xus.put(lane, NX + m, T(0));
+  xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
 }
 
 template <class T>
@@ -340,16 +438,38 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   }
 }
 
-// USE_CC: integrate the tangent from the captured linearisation scalars (fused small-batch
-// path: CC is slot-local and L2-resident) instead of re-evaluating f with sin/cos per stage
-// (split path: saves re-reading 80 scalars per stage from HBM).
-template <class T, bool USE_CC = false>
-__device__ __forceinline__ void forward_body(const SplitArgs<T>& a, const int64_t c) {
-  // Recomputes the nominal RK4 stages (one fused value+tangent pass, mpcb_model.h rk4<T,true>)
-  // instead of re-reading the 80 captured scalars: per stage it streams only xbar/ubar (16)
-  // and the gains (52), prefetched one stage ahead.
+// P3 LDS carve (dynamic): two stage images (XU | KR | CC) for the one-stage-ahead DMA, plus the
+// output-row staging of S stages x (X row | U row) per instance.  S is the largest that keeps
+// the residency each use needs: fp32 large chunks 4 waves/CU (<= 40 KiB), fp64 + CC <= 160 KiB.
+template <class T, bool USE_CC>
+struct FwdLds {
+  static constexpr int IN = (XU_REC + KR_REC + (USE_CC ? CCS_REC : 0)) * WAVE;
+  static constexpr int S = (sizeof(T) == 8) == USE_CC ? 1 : 4;
+  static constexpr int V = 16 / sizeof(T);
+  static constexpr int ROW = NX + NU;
+  static constexpr int RSTRIDE = S * ROW + V;
+  static constexpr size_t BYTES = (size_t)(2 * IN + WAVE * RSTRIDE) * sizeof(T);
+};
+
+// USE_CC: integrate the forward tangent from the captured linearisation scalars (small chunks:
+// CC is cache resident) instead of re-evaluating f with sin/cos (large chunks: saves streaming
+// 80 scalars per stage back from HBM).
+template <class T, bool USE_CC>
+__device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
+  using L = FwdLds<T, USE_CC>;
+  constexpr int S = L::S, V = L::V, ROW = L::ROW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  T* const img0 = reinterpret_cast<T*>(dyn_lds);
+  T* const img1 = img0 + L::IN;
+  T* const rows = img1 + L::IN;
+  const int lane = threadIdx.x;
   const int64_t nb = a.nb;
-  if (c >= nb) return;
+  const int64_t c0 = (int64_t)blockIdx.x * WAVE;
+  const bool valid = c0 + lane < nb;
+  const int64_t c = valid ? c0 + lane : nb - 1;
+  const int64_t nq = (nb + SS - 1) / SS;
+  const int nqv = (int)((nq - c0 / SS) < WQ ? nq - c0 / SS : WQ);
+  const int nvalid = (int)((nb - c0) < WAVE ? nb - c0 : WAVE);
   const int64_t b = a.b0 + c;
   const int N = a.N;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
@@ -357,83 +477,139 @@ __device__ __forceinline__ void forward_body(const SplitArgs<T>& a, const int64_
   if (a.wind) {
     w[0] = a.wind[b * a.wind_sb]; w[1] = a.wind[b * a.wind_sb + 1]; w[2] = a.wind[b * a.wind_sb + 2];
   }
-  T xb[NX], ub[NU], kr[KR_REC];
-  {
-    const T* xu = soa(a.XU, 0, XU_REC, nb, c);
-#pragma unroll
-    for (int i = 0; i < XU_REC; ++i) (i < NX ? xb[i] : ub[i - NX]) = xu[i * SS];
-    const T* k0 = soa(a.KR, 0, KR_REC, nb, c);
-#pragma unroll
-    for (int i = 0; i < KR_REC; ++i) kr[i] = k0[i * SS];
-  }
+  // LDS byte addresses of the two stage images (M0 operands of the DMA)
+  const unsigned lds0 = (unsigned)(size_t)(lds_void*)dyn_lds;
+  const unsigned lds1 = lds0 + L::IN * (unsigned)sizeof(T);
+  const bool dma_lane = Dma<T>::lane_valid(lane, nqv);
+  const int off_xu = Dma<T>::lane_offset(lane, XU_REC), off_kr = Dma<T>::lane_offset(lane, KR_REC),
+            off_cc = Dma<T>::lane_offset(lane, CCS_REC);
+  auto dma = [&](int k, unsigned im) {
+    if (dma_lane) {
+      dma_record<T, XU_REC>(im, soa(a.XU, k, XU_REC, nb, c0) + off_xu);
+      if (k < N) {
+        dma_record<T, KR_REC>(im + XU_REC * WAVE * sizeof(T), soa(a.KR, k, KR_REC, nb, c0) + off_kr);
+        if constexpr (USE_CC)
+          dma_record<T, CCS_REC>(im + (XU_REC + KR_REC) * WAVE * sizeof(T),
+                                 soa(a.CC, k, CCS_REC, nb, c0) + off_cc);
+      }
+    }
+  };
+  // rows [k0, k0 + NS) of X (and of U where < N) of the wave's valid instances
+  auto flush_rows = [&](int k0, auto ns_tag) {
+    constexpr int NS = decltype(ns_tag)::value, CX = NX / V, CU = NU / V;
+    const int64_t inst0 = a.b0 + c0;
+    // chunk t of X: instance t / (NS*CX), row (t % (NS*CX)) / CX, part t % CX
+    auto xsrc = [&](int t) {
+      const int l = t / (NS * CX), r = t - l * (NS * CX), sr = r / CX;
+      return rows + l * L::RSTRIDE + sr * ROW + (r - sr * CX) * V;
+    };
+    auto xdst = [&](int t) {
+      const int l = t / (NS * CX), r = t - l * (NS * CX);
+      return a.X + ((inst0 + l) * (N + 1) + k0) * NX + r * V;
+    };
+    auto usrc = [&](int t) {
+      const int l = t / (NS * CU), r = t - l * (NS * CU), sr = r / CU;
+      return rows + l * L::RSTRIDE + sr * ROW + NX + (r - sr * CU) * V;
+    };
+    auto udst = [&](int t) {
+      const int l = t / (NS * CU), r = t - l * (NS * CU);
+      return a.U + ((inst0 + l) * N + k0) * NU + r * V;
+    };
+    const bool do_u = a.U && k0 + NS <= N;
+    if (nvalid == WAVE) {
+      if (a.X) copy_chunks<NS * CX>(lane, xsrc, xdst);
+      if (do_u) copy_chunks<NS * CU>(lane, usrc, udst);
+    } else {
+      if (a.X)
+        for (int t = lane; t < nvalid * NS * CX; t += WAVE) copy16(xdst(t), xsrc(t));
+      if (do_u)
+        for (int t = lane; t < nvalid * NS * CU; t += WAVE) copy16(udst(t), usrc(t));
+    }
+  };
+  dma(0, lds0);
+  wait_vm();
   T dx[NX];
   {
     const T* x0 = a.x0 + b * a.x0_sb;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) dx[i] = iterate ? x0[i] - xb[i] : T(0);
+    for (int i = 0; i < NX; ++i) dx[i] = iterate ? x0[i] - img0[i * WAVE + lane] : T(0);
   }
   bool fin = true;
   for (int k = 0; k < N; ++k) {
-    // prefetch stage k+1
-    T xn[NX], un[NU], krn[KR_REC];
-    {
-      const T* xu = soa(a.XU, k + 1, XU_REC, nb, c);
+    T* const cur = (k & 1) ? img1 : img0;
+    T* const nxt = (k & 1) ? img0 : img1;
+    dma(k + 1, (k & 1) ? lds0 : lds1);
+    T gp[NX];
+    if (USE_CC && iterate) {
+      const T* g = soa(a.GP, k, GP_REC, nb, c);
 #pragma unroll
-      for (int i = 0; i < XU_REC; ++i) (i < NX ? xn[i] : un[i - NX]) = xu[i * SS];
-      if (k + 1 < N) {
-        const T* kp = soa(a.KR, k + 1, KR_REC, nb, c);
-#pragma unroll
-        for (int i = 0; i < KR_REC; ++i) krn[i] = kp[i * SS];
-      }
+      for (int i = 0; i < NX; ++i) gp[i] = g[i * SS];
     }
-    T du[NU];
+    T xb[NX], ub[NU], du[NU];
 #pragma unroll
-    for (int m = 0; m < NU; ++m) du[m] = kr[4 * NX + m];
+    for (int i = 0; i < NX; ++i) xb[i] = cur[i * WAVE + lane];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) ub[m] = cur[(NX + m) * WAVE + lane];
+    const T* kr = cur + XU_REC * WAVE + lane;
+#pragma unroll
+    for (int m = 0; m < NU; ++m) du[m] = kr[(4 * NX + m) * WAVE];
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
 #pragma unroll
-      for (int m = 0; m < NU; ++m) du[m] += kr[4 * i + m] * dx[i];
+      for (int m = 0; m < NU; ++m) du[m] += kr[(4 * i + m) * WAVE] * dx[i];
     }
-    if (a.X) {
-      T* Xo = a.X + (b * (N + 1) + k) * NX;
+    T* const row = rows + lane * L::RSTRIDE + (k % S) * ROW;
 #pragma unroll
-      for (int i = 0; i < NX; ++i) Xo[i] = xb[i] + dx[i];
-    }
-    if (a.U || k == 0) {
+    for (int i = 0; i < NX; ++i) row[i] = xb[i] + dx[i];
+    {
       T uo[NU];
 #pragma unroll
-      for (int m = 0; m < NU; ++m) { uo[m] = ub[m] + du[m]; fin = fin && (uo[m] - uo[m] == T(0)); }
-      if (a.U) store_vec<NU>(a.U + (b * N + k) * NU, uo);
-      if (k == 0) store_vec<NU>(a.u0 + b * NU, uo);
+      for (int m = 0; m < NU; ++m) {
+        uo[m] = ub[m] + du[m];
+        row[NX + m] = uo[m];
+        fin = fin && (uo[m] - uo[m] == T(0));
+      }
+      if (k == 0 && valid) store_vec<NU>(a.u0 + b * NU, uo);
     }
+    if (k % S == S - 1) flush_rows(k - (S - 1), std::integral_constant<int, S>());
     T phi[NX], dphi[NX];
     if constexpr (USE_CC) {
-      rk4_tan<T, false>(soa(a.CC, k, CCS_REC, nb, c), dx, du, a.h, a.M, dphi, SS);
-      if (iterate) {
-        const T* gp = soa(a.GP, k, GP_REC, nb, c);
-#pragma unroll
-        for (int i = 0; i < NX; ++i) phi[i] = gp[i * SS] + xn[i];
-      }
+      const T* cc = cur + (XU_REC + KR_REC) * WAVE + lane;
+      rk4_tan_g<T, false>([&](int i) { return cc[i * WAVE]; }, dx, du, a.h, a.M, dphi);
     } else {
       rk4<T, true>(xb, dx, ub, du, a.h, a.M, w, phi, dphi);
     }
+    wait_vm();          // stage k+1 image landed (and this stage's row stores drained)
+    if (iterate) {
 #pragma unroll
-    for (int i = 0; i < NX; ++i) dx[i] = iterate ? dphi[i] + (phi[i] - xn[i]) : dphi[i];
+      for (int i = 0; i < NX; ++i)
+        dx[i] = USE_CC ? dphi[i] + gp[i] : dphi[i] + (phi[i] - nxt[i * WAVE + lane]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NX; ++i) xb[i] = xn[i];
-#pragma unroll
-    for (int m = 0; m < NU; ++m) ub[m] = un[m];
-#pragma unroll
-    for (int i = 0; i < KR_REC; ++i) kr[i] = krn[i];
+      for (int i = 0; i < NX; ++i) dx[i] = dphi[i];
+    }
   }
-  if (a.X) {
-    T* Xo = a.X + (b * (N + 1) + N) * NX;
+  {
+    const T* last = (N & 1) ? img1 : img0;
+    T* const row = rows + lane * L::RSTRIDE + (N % S) * ROW;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) Xo[i] = xb[i] + dx[i];
+    for (int i = 0; i < NX; ++i) row[i] = last[i * WAVE + lane] + dx[i];
+    // rows N - N % S .. N: the terminal row and the unflushed tail, one row at a time
+    for (int k0 = N - N % S; k0 <= N; ++k0) {
+      if constexpr (S > 1) {
+        T* const src = rows + lane * L::RSTRIDE + (k0 % S) * ROW;
+        T* const dst = rows + lane * L::RSTRIDE;
+        if (k0 % S) {
+#pragma unroll
+          for (int i = 0; i < ROW; ++i) dst[i] = src[i];
+        }
+      }
+      flush_rows(k0, std::integral_constant<int, 1>());
+    }
   }
 #pragma unroll
   for (int i = 0; i < NX; ++i) fin = fin && (dx[i] - dx[i] == T(0));
-  if (!fin) a.status[b] = MPCB_STATUS_NAN;
+  if (valid && !fin) a.status[b] = MPCB_STATUS_NAN;
 }
 
 template <class T> int64_t split_elems_per_instance(int N, int iterate) {
@@ -441,13 +617,9 @@ template <class T> int64_t split_elems_per_instance(int N, int iterate) {
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) nominal_kernel(SplitArgs<T> a) {
-  nominal_body<T>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-}
+__global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_wave<T>(a); }
 template <class T, bool USE_CC>
-__global__ void __launch_bounds__(256) forward_kernel(SplitArgs<T> a) {
-  forward_body<T, USE_CC>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-}
+__global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_P2_WAVES_F32, 8)))
 riccati_kernel_f32(SplitArgs<float> a) { riccati_body<float>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4)); }
@@ -455,47 +627,23 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs
   riccati_body<double>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
-// Small batches: the same three bodies run back to back inside ONE wavefront per 4 instances
-// (grid-stride over the batch), on a per-wavefront slot of the workspace.  A 4096-instance
-// batch is 1024 wavefronts = one per SIMD, so this launch is latency-bound either way; fusing
-// removes the two dependent launch boundaries and keeps the workspace L2-resident.
-template <class T>
-__global__ void __launch_bounds__(64) fused_kernel(SplitArgs<T> a, int64_t B, int64_t slot_elems) {
-  const int lane = threadIdx.x, q = lane >> 4, j = lane & 15;
-  T* slot = a.XU + (int64_t)blockIdx.x * slot_elems;
-  SplitArgs<T> s = a;
-  const int N = a.N;
-  s.XU = slot;
-  s.CC = s.XU + (int64_t)(N + 1) * GROUPS * XU_REC;
-  s.KR = s.CC + (int64_t)N * GROUPS * CCS_REC;
-  s.GP = s.KR + (int64_t)N * GROUPS * KR_REC;
-  for (int64_t wave = blockIdx.x; wave * GROUPS < B; wave += gridDim.x) {
-    s.b0 = wave * GROUPS;
-    s.nb = (B - s.b0 < GROUPS) ? B - s.b0 : GROUPS;
-    if (j == 0) nominal_body<T>(s, q);
-    __syncthreads();
-    riccati_body<T>(s, q);
-    __syncthreads();
-    if (s.fwd && j == 0) forward_body<T, true>(s, q);
-    __syncthreads();
-  }
-}
-
-template <class T> int64_t fused_slot_elems(int N) {
-  return split_elems_per_instance<T>(N, 1) * GROUPS;
-}
-
-template <class T>
-hipError_t launch_fused(const SplitArgs<T>& a, int64_t B, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((fused_kernel<T>), dim3(grid), dim3(64), 0, st, a, B, fused_slot_elems<T>(a.N));
-  return hipGetLastError();
+template <class T, bool USE_CC>
+static hipError_t launch_forward(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
+  constexpr size_t bytes = FwdLds<T, USE_CC>::BYTES;
+  static_assert(bytes <= 160 * 1024, "P3 LDS carve exceeds the CU's 160 KiB");
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&forward_kernel<T, USE_CC>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((forward_kernel<T, USE_CC>), dim3(grid), dim3(WAVE), bytes, st, a);
+  return hipSuccess;
 }
 
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
-  const unsigned g256 = (unsigned)((a.nb + 255) / 256);
+  const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL((nominal_kernel<T>), dim3(g256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
   if constexpr (sizeof(T) == 4)
     hipLaunchKernelGGL(riccati_kernel_f32, dim3(g64), dim3(64), 0, st, a);
@@ -505,20 +653,12 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
-  if (a.fwd) {
-    if (a.nb <= 16384)
-      hipLaunchKernelGGL((forward_kernel<T, true>), dim3(g256), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((forward_kernel<T, false>), dim3(g256), dim3(256), 0, st, a);
-  }
+  hipError_t e = hipSuccess;
+  if (a.fwd) e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
   if (ev) (void)hipEventRecord(ev[3], st);
-  return hipGetLastError();
+  return e != hipSuccess ? e : hipGetLastError();
 }
 
-template hipError_t launch_fused<double>(const SplitArgs<double>&, int64_t, int, hipStream_t);
-template hipError_t launch_fused<float>(const SplitArgs<float>&, int64_t, int, hipStream_t);
-template int64_t fused_slot_elems<double>(int);
-template int64_t fused_slot_elems<float>(int);
 template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t, hipEvent_t*);
 template hipError_t launch_split<float>(const SplitArgs<float>&, hipStream_t, hipEvent_t*);
 template int64_t split_elems_per_instance<double>(int, int);
