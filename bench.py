@@ -111,7 +111,7 @@ def run(w, world, rank, dev, steps, warmup):
     from mpc_blaster_amd.dist import allreduce_histogram
     B, N = w['batch'], w['N']
     cfg = MPCConfig(N=N, dtype=w['dtype'], lbu=np.zeros(4) if w['box'] else None,
-                    ubu=np.full(4, 65.0) if w['box'] else None)
+                    ubu=np.full(4, 65.0) if w['box'] else None, max_as_iter=w.get('max_as_iter', 200))
     mpc = BatchedMPC(cfg, max_batch=B, device=dev)
     inp = mpc.gen_inputs(B, seed=w['seed'], id_offset=rank * B, ref=w['ref'], wind=w['wind'])
     torch.cuda.synchronize()
@@ -221,6 +221,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-secondary', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
+    ap.add_argument('--max-as-iter', type=int, default=200, help='active-set cap (box workload)')
     args = ap.parse_args()
 
     import torch
@@ -229,6 +230,7 @@ def main():
     w = dict(WORKLOADS[args.workload], name=args.workload)
     if args.batch:
         w['batch'] = args.batch
+    w['max_as_iter'] = args.max_as_iter
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))

@@ -144,7 +144,9 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   // (MPCB_SPLIT_MIN_BATCH above the batch), small unconstrained batches.
   int64_t split_min = 1;
   if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
-  h->split = (!cfg->box_u && max_batch >= split_min) ? 1 : 0;
+  h->split = (max_batch >= split_min) ? 1 : 0;
+  if (const char* e = getenv("MPCB_BOX_IMPL"))   // "v1": the single-kernel active-set solver
+    if (cfg->box_u && strcmp(e, "v1") == 0) h->split = 0;
   if (!h->split) {
     h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
     h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
@@ -156,7 +158,8 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     if (chunk < 64) chunk = 64;
     if (chunk > max_batch) chunk = max_batch;
     h->chunk = chunk;
-    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1) : split_elems_per_instance<float>(cfg->N, 1);
+    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, cfg->box_u)
+                            : split_elems_per_instance<float>(cfg->N, 1, cfg->box_u);
     h->chunk_elems = per * ((chunk + 3) / 4 * 4);
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
@@ -224,7 +227,8 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.wind = (const T*)wind; a.wind_sb = wind_sb;
     a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
-    a.fwd = (X || U || mode == MPCB_MODE_ITERATE) ? 1 : 0;
+    a.fwd = (X || U || mode == MPCB_MODE_ITERATE || h->cfg.box_u) ? 1 : 0;
+    a.max_as_iter = h->cfg.max_as_iter;
     const int N = h->cfg.N;
     int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
@@ -237,6 +241,10 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.CC = a.XU + (int64_t)(N + 1) * nbp * XU_REC;
       a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
       a.GP = a.KR + (int64_t)N * nbp * KR_REC;
+      a.AB = h->cfg.box_u ? a.GP + (int64_t)N * nbp * GP_REC : nullptr;
+      a.ABT = h->cfg.box_u ? a.AB + (int64_t)N * nbp * AB_REC : nullptr;
+      a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
+      a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));

@@ -56,6 +56,13 @@ template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipS
 //   GP [N][12][nb]      gap Phi(xbar_k, ubar_k) - xbar_{k+1}      (iterate mode only)
 //   KR [N][52][nb]      K_k (48, K[m][i] at row 4*i+m) | kff_k (4)
 constexpr int XU_REC = 16, CCS_REC = 80, GP_REC = 12, KR_REC = 52;
+// input-box path: column j of [A|B] at j*NX + i; input row m of the stage Hessian (16) + h_u[m]
+// Element orders put the 16 lanes of an instance on CONSECUTIVE elements for every access:
+//   AB  [A|B]_{ij} at i*16 + j (backward: lane j reads column j)
+//   ABT [A|B]_{ij} at j*12 + i (forward: state lane i reads row i)
+//   GH  input row m of the stage Hessian, entry i (16 = h_u) at i*4 + m
+//   PS  P_k column j entry i (12 = p_k[j]) at i*12 + j
+constexpr int AB_REC = 12 * 16, GH_REC = 4 * 17, PS_REC = 12 * 13;
 
 template <class T>
 struct SplitArgs {
@@ -73,12 +80,16 @@ struct SplitArgs {
   const T* xbar; const T* ubar;
   T* u0; T* X; T* U; int32_t* status;
   T* XU; T* CC; T* GP; T* KR;
+  T* AB; T* ABT; T* GH;   // box path: P2 exports the linearisation and the Hessian's input rows
+  T* PS;             // box path: value-function snapshots for restarts
+  int max_as_iter;
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
                                            hipEvent_t* ev = nullptr);
-template <class T> int64_t split_elems_per_instance(int N, int iterate);  // per 64-padded instance
+template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st);
+template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance
 template <class T> int64_t solve_slot_elems(int N, int box);
 
 template <class T>

@@ -379,19 +379,19 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
         // V = {free u<lb} U {free u>ub} U {at lb, mu<0} U {at ub, mu>0}; |V| = 0 <=> KKT.
         const uint64_t V = vlo | vhi | vfl | vfu;
         int cnt = (j >= NX) ? __popcll(V) : 0;
-        int lastk = (j >= NX && V) ? (63 - __clzll(V)) * NU + ju : -1;
-        int nV = 0, last = -1;
+        int firstk = (j >= NX && V) ? __ffsll((long long)V) - 1 : 64;
+        int nV = 0, first = 64 * NU;
 #pragma unroll
         for (int m = 0; m < NU; ++m) {
           nV += __shfl(cnt, q * 16 + NX + m);
-          const int lm = __shfl(lastk, q * 16 + NX + m);
-          last = lm > last ? lm : last;
+          const int fm = __shfl(firstk, q * 16 + NX + m) * NU + m;
+          first = fm < first ? fm : first;
         }
         const bool gconv = nV == 0;
         const bool full = (nV < best) || (pcount > 0);
         pcount = (nV < best) ? 3 : (full ? pcount - 1 : pcount);
         best = nV < best ? nV : best;
-        uint64_t selm = full ? V : ((last >= 0 && (last % NU) == ju && j >= NX) ? (1ull << (last / NU)) : 0ull);
+        uint64_t selm = full ? V : ((first < 64 * NU && (first % NU) == ju && j >= NX) ? (1ull << (first / NU)) : 0ull);
         const uint64_t nlow = (sel<NU>(low, ju) | (selm & vlo)) & ~(selm & vfl);
         const uint64_t nup = (sel<NU>(up, ju) | (selm & vhi)) & ~(selm & vfu);
         const bool gchanged = !gconv;

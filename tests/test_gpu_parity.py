@@ -188,8 +188,10 @@ def test_phase_timing_events(path, box):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert t['riccati'] > 0
-    if m.path == 'split':
+    if m.path == 'split' and not box:
         assert t['nominal'] > 0 and t['forward'] < t['riccati']   # u0 only: no forward kernel
+    elif box:
+        assert t['nominal'] > 0 and t['forward'] > 0              # active-set kernel
     else:
         assert t['nominal'] == 0 and t['forward'] == 0
 
