@@ -222,6 +222,39 @@ def test_full_size_c3_properties():
     assert relerr(X[idx].cpu().numpy(), o['X']).max() < 5e-5
 
 
+def test_full_size_c4_box_properties():
+    """BASELINE c4 per-GPU shard (65536, N=30, fp32, thrust box [0, 65]): every instance reaches
+    its KKT point (no MAXITER), bounds hold, sampled oracle parity, and the single-kernel
+    active-set solver (MPCB_BOX_IMPL=v1) agrees on a slice."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    B, N = 65536, 30
+    cfg = MPCConfig(N=N, dtype='f32', lbu=np.zeros(4), ubu=np.full(4, 65.0))
+    m = BatchedMPC(cfg, max_batch=B)
+    d = m.gen_inputs(B, seed=1004, ref='hover')
+    u0 = m.solve(d['x0'], d['xref'], d['uref'], want_traj=True).clone()
+    U = m.get_input_trajectory().clone()
+    st = m.get_status().clone()
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert (U >= -1e-4).all() and (U <= 65 + 1e-3).all()
+    idx = np.arange(0, B, 2731)
+    x0 = d['x0'][idx].double().cpu().numpy()
+    xr = np.broadcast_to(d['xref'][0].double().cpu().numpy(), (len(idx), N + 1, 12)).copy()
+    o = mpc_solve(x0, xr, np.full((len(idx), N, 4), np.float32(22.0725), dtype=np.float64), _spec(N, box=True))
+    assert (o['status'] == 0).all()
+    assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-5
+    assert relerr(U[idx].cpu().numpy(), o['U']).max() < 5e-5
+    os.environ['MPCB_BOX_IMPL'] = 'v1'
+    try:
+        m1 = BatchedMPC(cfg, max_batch=512)
+    finally:
+        os.environ.pop('MPCB_BOX_IMPL')
+    assert m1.path == 'fused'
+    u1 = m1.solve(d['x0'][:512], d['xref'], d['uref'], want_traj=False)
+    torch.cuda.synchronize()
+    assert relerr(u1.cpu().numpy(), u0[:512].cpu().numpy()).max() < 5e-5
+
+
 def test_closed_loop_matches_oracle_fp64():
     """Receding-horizon loop (simulation_blaster.py:56-107) with the persistent SQP_RTI iterate."""
     from mpc_blaster_amd.closed_loop import closed_loop
