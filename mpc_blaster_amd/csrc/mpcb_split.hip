@@ -175,7 +175,9 @@ __device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
   xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
 }
 
-template <class T>
+// EXPORT (input-box path): also store column j of [A|B] and the input rows of the stage Hessian
+// for the active-set kernel (a separate instantiation keeps the plain pass's registers lean)
+template <class T, bool EXPORT>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
@@ -250,7 +252,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
-      if (a.AB && valid) {
+      if (EXPORT && valid) {
         T* ab = soa(a.AB, k, AB_REC, nb, c);
         T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
@@ -317,7 +319,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       }
       hj += s * acc;
     }
-    if (a.GH && valid && j >= NX) {
+    if (EXPORT && valid && j >= NX) {
       T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
@@ -579,10 +581,14 @@ __global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_w
 template <class T, bool USE_CC>
 __global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
+template <bool EXPORT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_P2_WAVES_F32, 8)))
-riccati_kernel_f32(SplitArgs<float> a) { riccati_body<float>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4)); }
+riccati_kernel_f32(SplitArgs<float> a) {
+  riccati_body<float, EXPORT>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+}
+template <bool EXPORT>
 __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs<double> a) {
-  riccati_body<double>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  riccati_body<double, EXPORT>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
 template <class T, bool USE_CC>
@@ -603,10 +609,13 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(riccati_kernel_f32, dim3(g64), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(riccati_kernel_f64, dim3(g64), dim3(64), 0, st, a);
+  if constexpr (sizeof(T) == 4) {
+    if (a.AB) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
+  } else {
+    if (a.AB) hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(riccati_kernel_f64<false>, dim3(g64), dim3(64), 0, st, a);
+  }
   if (ev) (void)hipEventRecord(ev[2], st);
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
