@@ -197,6 +197,15 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   const T* xr = a.xref + b * a.xref_sb;
   const T* ur = a.uref + b * a.uref_sb;
 
+  // s * blkdiag(Q, R) in LDS: lane j reads column j (= row j), so the stage-cost terms are the
+  // same instruction stream in state and input lanes (no divergent branch per stage)
+  __shared__ __attribute__((aligned(16))) T SW[NZ * NZ];
+  for (int e = lane; e < NZ * NZ; e += 64) {
+    const int r = e / NZ, cl = e % NZ;
+    const T wq = (r < NX && cl < NX) ? W.Q[r * NX + cl] : T(0);
+    const T wr = (r >= NX && cl >= NX) ? W.R[(r - NX) * NU + (cl - NX)] : T(0);
+    SW[e] = s * (wq + wr);
+  }
   T pj;      // p_{k+1}[j]
   T Pc[NX];  // column j of P_{k+1} (zero in the input lanes: P padded to 16x16)
   {
@@ -252,7 +261,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
-      if (EXPORT && valid) {
+      if (EXPORT && a.AB && valid) {
         T* ab = soa(a.AB, k, AB_REC, nb, c);
         T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
@@ -302,24 +311,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
         G[i] = acc;
       }
     }
-    {
-      T acc = T(0);
-      if (j < NX) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          G[i] += s * W.Q[i * NX + jx];
-          acc += W.Q[jx * NX + i] * L.v[i];
-        }
-      } else {
-#pragma unroll
-        for (int n = 0; n < NU; ++n) {
-          G[NX + n] += s * W.R[n * NU + ju];
-          acc += W.R[ju * NU + n] * L.v[NX + n];
-        }
-      }
-      hj += s * acc;
+    for (int i = 0; i < NZ; ++i) {
+      const T w = SW[j * NZ + i];
+      G[i] += w;
+      hj += w * L.v[i];
     }
-    if (EXPORT && valid && j >= NX) {
+    if (EXPORT && a.AB && valid && j >= NX) {
       T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
@@ -370,19 +368,23 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     kff0 = sel<NU>(kff, ju);
     __syncthreads();
-    // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_solve.hip)
-    if (j < NX) {
+    // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_solve.hip).  Every
+    // lane publishes its column and takes the entries below its diagonal from the lanes that
+    // own them: uniform code instead of per-entry predicated stores.  (L.X is free: this
+    // stage's products are done.)
 #pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        if (i <= j) L.P[j * NX + i] = Pn[i];
-        if (i < j) L.P[i * NX + j] = Pn[i];
-      }
-    }
+    for (int i = 0; i < NX; ++i) L.X[j * NX + i] = Pn[i];
     pj = pn;
     if (k > 0) commit(buf ^ 1);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? L.P[jx * NX + i] : T(0);
+    for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
+    if constexpr (sizeof(T) == 8) {   // the fp64 products read P from LDS
+      if (j < NX) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) L.P[j * NX + i] = Pc[i];
+      }
+    }
     buf ^= 1;
     cyb = pyb;
     cyr = pyr;
@@ -613,8 +615,9 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     if (a.AB) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
     else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
   } else {
-    if (a.AB) hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(riccati_kernel_f64<false>, dim3(g64), dim3(64), 0, st, a);
+    // one fp64 instantiation (export guarded at run time): measured leaner than the export-free
+    // one, which LLVM schedules into 368 bytes of scratch spill
+    hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
