@@ -229,20 +229,21 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   // Stage data is prefetched one stage ahead into registers (5 linearisation scalars, the own
   // component of ybar and yref, one gap value per lane) and committed to a double-buffered LDS
   // copy, so the tangent integrates from LDS and no global-load latency sits on the chain.
-  __shared__ T Cst[2][GROUPS][CCS_REC + GP_REC];
+  // (every lane loads and commits through one address select: no divergent branch)
+  __shared__ T Cst[2][GROUPS][CCS_REC + NZ];
   T pc[5], pyb, pyr, pgp = T(0);
   auto prefetch = [&](int k) {
     const T* cc = soa(a.CC, k, CCS_REC, nb, c);
 #pragma unroll
     for (int r = 0; r < 5; ++r) pc[r] = cc[(j + 16 * r) * SS];
     pyb = soa(a.XU, k, XU_REC, nb, c)[j * SS];
-    pyr = (j < NX) ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju];
-    if (iterate && j < NX) pgp = soa(a.GP, k, GP_REC, nb, c)[j * SS];
+    pyr = *((j < NX) ? xr + (int64_t)k * NX + jx : ur + (int64_t)k * NU + ju);
+    if (iterate) pgp = soa(a.GP, k, GP_REC, nb, c)[jx * SS];   // input lanes: unused copy
   };
   auto commit = [&](int bufi) {
 #pragma unroll
     for (int r = 0; r < 5; ++r) Cst[bufi][q][j + 16 * r] = pc[r];
-    if (j < NX) Cst[bufi][q][CCS_REC + j] = pgp;
+    Cst[bufi][q][CCS_REC + j] = pgp;
   };
   prefetch(N - 1);
   commit(0);
@@ -357,16 +358,17 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
       Pn[i] = acc;
     }
+    kff0 = sel<NU>(kff, ju);
     if (valid) {
+      // K[m][j] at 4j + m (state lanes), kff[m] at 4*NX + m (input lanes): the first store is
+      // common to both kinds of lane
       T* kr = soa(a.KR, k, KR_REC, nb, c);
+      kr[((j < NX) ? 4 * j : 4 * NX + ju) * SS] = (j < NX) ? Kj[0] : kff0;
       if (j < NX) {
 #pragma unroll
-        for (int m = 0; m < NU; ++m) kr[(4 * j + m) * SS] = Kj[m];
-      } else {
-        kr[(4 * NX + ju) * SS] = sel<NU>(kff, ju);
+        for (int m = 1; m < NU; ++m) kr[(4 * j + m) * SS] = Kj[m];
       }
     }
-    kff0 = sel<NU>(kff, ju);
     __syncthreads();
     // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_solve.hip).  Every
     // lane publishes its column and takes the entries below its diagonal from the lanes that
