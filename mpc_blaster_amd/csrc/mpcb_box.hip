@@ -28,7 +28,9 @@ namespace mpcb {
 #define MPCB_BOX_WAVES 2
 #endif
 
-template <class T>
+// BOX = false: the same passes for the unconstrained QP of small batches (one backward pass over
+// the [A|B] the parallel linearisation kernel cached, one forward pass; no active set).
+template <class T, bool BOX>
 __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
@@ -72,7 +74,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       const int o = __shfl(kc, g * 16);
       kmax = o > kmax ? o : kmax;
     }
-    if (it > 0 && kmax >= 0) {
+    if ((it > 0 || !BOX) && kmax >= 0) {
       T pj = T(0);
       T Pc[NX];
       {
@@ -182,7 +184,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
           }
           hj += s * acc;
         }
-        if (act && valid && j >= NX) {   // unmasked input rows: the forward pass's multipliers
+        if (BOX && act && valid && j >= NX) {   // unmasked input rows: the forward's multipliers
           T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
           for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
@@ -201,7 +203,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
           ht[m] = L.hv[NX + m];
           Hux_t[m] = G[NX + m];
         }
-        {
+        if constexpr (BOX) {
           // fixed components: du_m = delta_m (bound - ubar), row/column m of H_uu -> identity
           const T* ub = ubk;
           bool fixed[NU];
@@ -276,7 +278,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? L.P[jx * NX + i] : T(0);
-        if (act && valid && j < NX && k > 0) {   // snapshot P_k, p_k for a later restart
+        if (BOX && act && valid && j < NX && k > 0) {   // snapshot P_k, p_k for a later restart
           T* ps = soa(a.PS, k, PS_REC, nb, c) + j * SS;
 #pragma unroll
           for (int i = 0; i < NX; ++i) ps[i * NX * SS] = Pc[i];
@@ -297,9 +299,11 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     auto fload = [&](int k) {
       fyb = soa(a.XU, k, XU_REC, nb, c)[j * SS];
       if (j >= NX) {
-        const T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
+        if constexpr (BOX) {
+          const T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
-        for (int i = 0; i <= NZ; ++i) fa[i] = gh[i * NU * SS];
+          for (int i = 0; i <= NZ; ++i) fa[i] = gh[i * NU * SS];
+        }
         const T* kr = soa(a.KR, k, KR_REC, nb, c);
 #pragma unroll
         for (int i = 0; i < NX; ++i) fb[i] = kr[(4 * i + ju) * SS];
@@ -341,6 +345,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         const T uk = yb + du;
         if (write && a.U) a.U[(b * N + k) * NU + ju] = uk;
         if (write && k == 0) a.u0[b * NU + ju] = uk;
+        if constexpr (BOX) {
         T mu = ra[NZ], mabs = fabs(ra[NZ]);
 #pragma unroll
         for (int i = 0; i < NZ; ++i) {
@@ -355,6 +360,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         vhi |= (uint64_t)(fr && uk > ubm + tol_u) << k;
         vfl |= (uint64_t)(lo && mu < -tol_mu) << k;
         vfu |= (uint64_t)(hi && mu > tol_mu) << k;
+        }
       } else {
         if (write && a.X) a.X[(b * (N + 1) + k) * NX + jx] = yb + dxj;
         T acc = ra[NZ];
@@ -366,6 +372,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     }
     if (write && a.X && j < NX) a.X[(b * (N + 1) + N) * NX + jx] = soa(a.XU, N, XU_REC, nb, c)[jx * SS] + dxj;
 
+    if constexpr (!BOX) break;
     // ------------------------------------------------ active-set update (Kim-Park)
     const uint64_t V = vlo | vhi | vfl | vfu;
     const int cnt = (j >= NX) ? __popcll(V) : 0;
@@ -413,27 +420,78 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
 #pragma unroll
     for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
     // the QP status of the unconstrained pass (P2 wrote it) carries over
-    const int32_t st0 = a.status[b];
+    const int32_t st0 = BOX ? a.status[b] : MPCB_STATUS_OK;
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
   }
 }
 
 // fp32 register budget: MPCB_BOX_WAVES waves per SIMD (latency-bound: the iterations of one
 // wave are serial, so co-resident waves are what hides the barrier / LDS / MFMA latencies)
+template <bool BOX>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_BOX_WAVES, 8)))
-box_kernel_f32(SplitArgs<float> a) { box_body<float>(a); }
-__global__ void __launch_bounds__(64) box_kernel_f64(SplitArgs<double> a) { box_body<double>(a); }
+box_kernel_f32(SplitArgs<float> a) { box_body<float, BOX>(a); }
+template <bool BOX>
+__global__ void __launch_bounds__(64) box_kernel_f64(SplitArgs<double> a) { box_body<double, BOX>(a); }
 
 template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f32<true>, dim3(g), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL(box_kernel_f64, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f64<true>, dim3(g), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---- small unconstrained batches -------------------------------------------------------------
+// The Riccati pass of the split path integrates 16 RK4 tangents per stage inside its serial
+// backward recursion; at a few thousand instances (c2: 4096, one wavefront per SIMD) that
+// recursion is latency-bound.  Here the tangents move to a fully parallel kernel over
+// (instance quad, stage) that caches [A_k | B_k] (AB and ABT orders), and the serial passes run
+// the Riccati algebra only (box_body<T, false>).
+template <class T>
+__global__ void __launch_bounds__(64) lin_kernel(SplitArgs<T> a) {
+  __shared__ T cc[CCS_REC * SS];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4;
+  const int j = lane & 15;
+  const int k = blockIdx.y;
+  const int64_t nb = a.nb;
+  const int64_t q0 = blockIdx.x;                 // instance quad
+  const int64_t nq = (nb + SS - 1) / SS;
+  if (q0 >= nq) return;
+  // the quad's stage-k capture is contiguous: 80 x 4 elements
+  const T* src = soa(a.CC, k, CCS_REC, nb, q0 * SS);
+  for (int e = lane; e < CCS_REC * SS; e += 64) cc[e] = src[e];
+  __syncthreads();
+  T dx[NX], du[NU], col[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
+#pragma unroll
+  for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
+  rk4_tan_g<T, false>([&](int i) { return cc[i * SS + q]; }, dx, du, a.h, a.M, col);
+  const int64_t c = q0 * SS + q;
+  T* ab = soa(a.AB, k, AB_REC, nb, c);
+  T* abt = soa(a.ABT, k, AB_REC, nb, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    ab[(i * NZ + j) * SS] = col[i];
+    abt[(j * NX + i) * SS] = col[i];
+  }
+}
+
+template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st) {
+  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  hipLaunchKernelGGL((lin_kernel<T>), dim3(g, a.N), dim3(64), 0, st, a);
+  if constexpr (sizeof(T) == 4)
+    hipLaunchKernelGGL(box_kernel_f32<false>, dim3(g), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(box_kernel_f64<false>, dim3(g), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
 template hipError_t launch_box<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_box<float>(const SplitArgs<float>&, hipStream_t);
+template hipError_t launch_small<double>(const SplitArgs<double>&, hipStream_t);
+template hipError_t launch_small<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb

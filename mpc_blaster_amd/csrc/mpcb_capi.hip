@@ -60,6 +60,7 @@ struct mpcb_handle {
   int64_t slot_elems;
   int64_t scratch_bytes;
   int split;              // 1: three-kernel split path; 0: single-kernel solver (boxes)
+  int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -158,8 +159,15 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     if (chunk < 64) chunk = 64;
     if (chunk > max_batch) chunk = max_batch;
     h->chunk = chunk;
-    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, cfg->box_u)
-                            : split_elems_per_instance<float>(cfg->N, 1, cfg->box_u);
+    // optional (MPCB_SMALL_MAX): linearise all stages in parallel and run the Riccati recursion
+    // over the cached [A|B].  Measured slower at c2 (lin 62 + passes 172 us vs P2+P3 187 us):
+    // the recursion's latency is its LDS exchanges, not the tangents, so it is off by default.
+    int64_t small_max = 0;
+    if (const char* e = getenv("MPCB_SMALL_MAX")) small_max = atoll(e);
+    h->small = (!cfg->box_u && chunk <= small_max) ? 1 : 0;
+    const int ab = cfg->box_u ? 2 : (h->small ? 1 : 0);
+    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
+                            : split_elems_per_instance<float>(cfg->N, 1, ab);
     h->chunk_elems = per * ((chunk + 3) / 4 * 4);
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
@@ -241,8 +249,9 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.CC = a.XU + (int64_t)(N + 1) * nbp * XU_REC;
       a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
       a.GP = a.KR + (int64_t)N * nbp * KR_REC;
-      a.AB = h->cfg.box_u ? a.GP + (int64_t)N * nbp * GP_REC : nullptr;
-      a.ABT = h->cfg.box_u ? a.AB + (int64_t)N * nbp * AB_REC : nullptr;
+      a.small = h->small;
+      a.AB = (h->cfg.box_u || h->small) ? a.GP + (int64_t)N * nbp * GP_REC : nullptr;
+      a.ABT = (h->cfg.box_u || h->small) ? a.AB + (int64_t)N * nbp * AB_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;

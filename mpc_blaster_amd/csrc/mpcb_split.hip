@@ -577,7 +577,7 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
 
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box) {
   return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR_REC + (iterate ? GP_REC : 0)) +
-         (box ? (int64_t)N * (2 * AB_REC + GH_REC + PS_REC) : 0);
+         (box == 2 ? (int64_t)N * (2 * AB_REC + GH_REC + PS_REC) : box == 1 ? (int64_t)N * 2 * AB_REC : 0);
 }
 
 template <class T>
@@ -613,6 +613,12 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
+  if (a.small) {   // linearisation + Riccati + forward over the cached [A|B] (mpcb_box.hip)
+    hipError_t e = launch_small<T>(a, st);
+    if (ev) (void)hipEventRecord(ev[2], st);
+    if (ev) (void)hipEventRecord(ev[3], st);
+    return e != hipSuccess ? e : hipGetLastError();
+  }
   if constexpr (sizeof(T) == 4) {
     if (a.AB) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
     else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);

@@ -23,21 +23,29 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 
 
+_PATH_ENV = {   # path -> library overrides (the defaults pick by batch size)
+    'split': {'MPCB_SPLIT_MIN_BATCH': '1'},                          # nominal / Riccati / forward
+    'small': {'MPCB_SPLIT_MIN_BATCH': '1', 'MPCB_SMALL_MAX': '1000000'},  # cached-[A|B] passes
+    'fused': {'MPCB_SPLIT_MIN_BATCH': str(1 << 40)},               # single-kernel solver
+}
+
+
 def _mpc(N, dtype='f64', box=False, max_batch=4096, path=None, **kw):
-    """path: None (library default by batch size), 'split' or 'fused' (forced via env)."""
+    """path: None (library default by batch size) or a key of _PATH_ENV (forced via env)."""
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     cfg = MPCConfig(N=N, dtype=dtype, lbu=np.zeros(4) if box else None,
                     ubu=np.full(4, 65.0) if box else None, **kw)
-    old = os.environ.get('MPCB_SPLIT_MIN_BATCH')
-    if path is not None:
-        os.environ['MPCB_SPLIT_MIN_BATCH'] = '1' if path == 'split' else str(1 << 40)
+    env = _PATH_ENV.get(path, {})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return BatchedMPC(cfg, max_batch=max_batch)
     finally:
-        if old is None:
-            os.environ.pop('MPCB_SPLIT_MIN_BATCH', None)
-        else:
-            os.environ['MPCB_SPLIT_MIN_BATCH'] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _spec(N, box=False):
@@ -99,6 +107,7 @@ def test_c1_golden_fp64():
     ('c3', 20, 'f32', False, 'fused'), ('c2', 10, 'f32', False, 'fused'),
     ('c2', 20, 'f64', False, 'split'), ('c3', 20, 'f64', False, 'split'),
     ('c3', 20, 'f32', False, 'split'), ('c2', 10, 'f32', False, 'split'),
+    ('c2', 20, 'f64', False, 'small'), ('c3', 20, 'f32', False, 'small'),
     ('c4', 30, 'f64', True, None), ('c4', 30, 'f32', True, None),
 ])
 def test_solve_matches_oracle(cfg, N, dtype, box, path):
@@ -123,7 +132,7 @@ def test_solve_matches_oracle(cfg, N, dtype, box, path):
         assert (U >= -1e-6).all() and (U <= 65 + 1e-4).all()
 
 
-@pytest.mark.parametrize('path', ['fused', 'split'])
+@pytest.mark.parametrize('path', ['fused', 'split', 'small'])
 def test_iterate_mode_matches_oracle_fp64(path):
     """acados SQP_RTI semantics: linearise at a given iterate with gaps and dx0 != 0."""
     N, B = 12, 41
@@ -139,7 +148,7 @@ def test_iterate_mode_matches_oracle_fp64(path):
     assert relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max() < 1e-9
 
 
-@pytest.mark.parametrize('path', ['fused', 'split'])
+@pytest.mark.parametrize('path', ['fused', 'split', 'small'])
 def test_wind_extension_fp64(path):
     N, B = 8, 16
     inp = make_inputs('c5', ids=np.arange(B, dtype=np.uint64), N=N)
@@ -164,7 +173,7 @@ def test_sim_step_and_histogram():
     assert np.array_equal(counts, ref)
 
 
-@pytest.mark.parametrize('path', ['fused', 'split'])
+@pytest.mark.parametrize('path', ['fused', 'split', 'small'])
 def test_u0_only_path_equals_full_path(path):
     N, B = 20, 64
     inp = make_inputs('c3', ids=np.arange(B, dtype=np.uint64), N=N)
@@ -175,7 +184,7 @@ def test_u0_only_path_equals_full_path(path):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('path,box', [('fused', False), ('split', False), (None, True)])
+@pytest.mark.parametrize('path,box', [('fused', False), ('split', False), ('small', False), (None, True)])
 def test_phase_timing_events(path, box):
     """mpcb_set_timing / mpcb_last_timing: per-phase device ms, and timing changes no result."""
     N, B = 20, 256
