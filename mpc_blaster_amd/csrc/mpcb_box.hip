@@ -28,10 +28,14 @@ namespace mpcb {
 #define MPCB_BOX_WAVES 2
 #endif
 
-// BOX = false: the same passes for the unconstrained QP of small batches (one backward pass over
-// the [A|B] the parallel linearisation kernel cached, one forward pass; no active set).
-template <class T, bool BOX>
+// MODE (the same passes serve three uses):
+//   PASS_BOX   input boxes: active-set iterations (the first backward pass is P2's)
+//   PASS_SMALL unconstrained, [A|B] cached by lin_kernel: one backward and one forward pass
+//   PASS_FWD   unconstrained, P2 already made the backward pass (and cached [A|B]^T): forward only
+enum { PASS_BOX = 1, PASS_SMALL = 0, PASS_FWD = 2 };
+template <class T, int MODE>
 __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
+  constexpr bool BOX = MODE == PASS_BOX;
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
   const int q = lane >> 4;
@@ -74,13 +78,13 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       const int o = __shfl(kc, g * 16);
       kmax = o > kmax ? o : kmax;
     }
-    if ((it > 0 || !BOX) && kmax >= 0) {
+    if ((BOX ? it > 0 : MODE == PASS_SMALL) && kmax >= 0) {
       T pj = T(0);
       T Pc[NX];
       {
         const T xN = soa(a.XU, N, XU_REC, nb, c)[jx * SS];
         L.v[j] = (j < NX) ? xN - xr[(int64_t)N * NX + jx] : T(0);
-        __syncthreads();
+        wave_lds_sync();
         if (kc == N - 1) {
           T acc = T(0);
 #pragma unroll
@@ -98,7 +102,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
 #pragma unroll
           for (int i = 0; i < NX; ++i) L.P[j * NX + i] = Pc[i];
         }
-        __syncthreads();
+        wave_lds_sync();
       }
       bool qp_ok = true;
       // stage data prefetched one stage ahead: column j of [A|B], own (ybar - yref) component,
@@ -138,7 +142,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
 #pragma unroll
           for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
         }
-        __syncthreads();
+        wave_lds_sync();
         T hj = T(0);
 #pragma unroll
         for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
@@ -192,9 +196,9 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         }
 #pragma unroll
         for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
-        __syncthreads();
+        wave_lds_sync();
         L.hv[j] = hj;
-        __syncthreads();
+        wave_lds_sync();
         T Ht[NU * NU], ht[NU], Hux_t[NU];
 #pragma unroll
         for (int m = 0; m < NU; ++m) {
@@ -266,7 +270,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
             kr[(4 * NX + ju) * SS] = sel<NU>(kff, ju);
           }
         }
-        __syncthreads();
+        wave_lds_sync();
         if (act && j < NX) {   // symmetric by construction (see riccati_body)
 #pragma unroll
           for (int i = 0; i < NX; ++i) {
@@ -275,7 +279,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
           }
         }
         if (act) pj = pn;
-        __syncthreads();
+        wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? L.P[jx * NX + i] : T(0);
         if (BOX && act && valid && j < NX && k > 0) {   // snapshot P_k, p_k for a later restart
@@ -325,7 +329,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       const T yb = fyb;
       if (k + 1 < N) fload(k + 1);
       L.v[j] = dxj;   // input lanes overwrite their slot with du below
-      __syncthreads();
+      wave_lds_sync();
       const bool lo = (sel<NU>(low, ju) >> k) & 1ull, hi = (sel<NU>(up, ju) >> k) & 1ull;
       if (j >= NX) {
         T du = rb[NX];
@@ -334,9 +338,9 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         // fixed components: the masked recursion set kff = delta and a zero gain row
         dxj = du;
       }
-      __syncthreads();
+      wave_lds_sync();
       if (j >= NX) L.v[j] = dxj;
-      __syncthreads();
+      wave_lds_sync();
       T z[NZ];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) z[i] = L.v[i];
@@ -368,7 +372,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         for (int l = 0; l < NZ; ++l) acc += ra[l] * z[l];
         dxj = acc;
       }
-      __syncthreads();
+      wave_lds_sync();
     }
     if (write && a.X && j < NX) a.X[(b * (N + 1) + N) * NX + jx] = soa(a.XU, N, XU_REC, nb, c)[jx * SS] + dxj;
 
@@ -420,25 +424,25 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
 #pragma unroll
     for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
     // the QP status of the unconstrained pass (P2 wrote it) carries over
-    const int32_t st0 = BOX ? a.status[b] : MPCB_STATUS_OK;
+    const int32_t st0 = MODE != PASS_SMALL ? a.status[b] : MPCB_STATUS_OK;
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
   }
 }
 
 // fp32 register budget: MPCB_BOX_WAVES waves per SIMD (latency-bound: the iterations of one
 // wave are serial, so co-resident waves are what hides the barrier / LDS / MFMA latencies)
-template <bool BOX>
+template <int MODE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_BOX_WAVES, 8)))
-box_kernel_f32(SplitArgs<float> a) { box_body<float, BOX>(a); }
-template <bool BOX>
-__global__ void __launch_bounds__(64) box_kernel_f64(SplitArgs<double> a) { box_body<double, BOX>(a); }
+box_kernel_f32(SplitArgs<float> a) { box_body<float, MODE>(a); }
+template <int MODE>
+__global__ void __launch_bounds__(64) box_kernel_f64(SplitArgs<double> a) { box_body<double, MODE>(a); }
 
 template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32<true>, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f32<PASS_BOX>, dim3(g), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL(box_kernel_f64<true>, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f64<PASS_BOX>, dim3(g), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -483,9 +487,19 @@ template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   hipLaunchKernelGGL((lin_kernel<T>), dim3(g, a.N), dim3(64), 0, st, a);
   if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32<false>, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f32<PASS_SMALL>, dim3(g), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL(box_kernel_f64<false>, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(box_kernel_f64<PASS_SMALL>, dim3(g), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+// forward pass of the plain split path in the 16-lane layout, from P2's gains and [A|B]^T
+template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st) {
+  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  if constexpr (sizeof(T) == 4)
+    hipLaunchKernelGGL(box_kernel_f32<PASS_FWD>, dim3(g), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(box_kernel_f64<PASS_FWD>, dim3(g), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -493,5 +507,7 @@ template hipError_t launch_box<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_box<float>(const SplitArgs<float>&, hipStream_t);
 template hipError_t launch_small<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_small<float>(const SplitArgs<float>&, hipStream_t);
+template hipError_t launch_fwd16<double>(const SplitArgs<double>&, hipStream_t);
+template hipError_t launch_fwd16<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb

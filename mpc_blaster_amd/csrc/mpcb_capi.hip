@@ -61,6 +61,7 @@ struct mpcb_handle {
   int64_t scratch_bytes;
   int split;              // 1: three-kernel split path; 0: single-kernel solver (boxes)
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
+  int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -165,7 +166,12 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     int64_t small_max = 0;
     if (const char* e = getenv("MPCB_SMALL_MAX")) small_max = atoll(e);
     h->small = (!cfg->box_u && chunk <= small_max) ? 1 : 0;
-    const int ab = cfg->box_u ? 2 : (h->small ? 1 : 0);
+    // small chunks: the forward pass in the 16-lane layout from P2's exported [A|B]^T (the
+    // thread-per-instance pass is latency-bound at a few thousand instances)
+    int64_t fwd16_max = 16384;
+    if (const char* e = getenv("MPCB_FWD16_MAX")) fwd16_max = atoll(e);
+    h->fwd16 = (!cfg->box_u && !h->small && chunk <= fwd16_max) ? 1 : 0;
+    const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
     h->chunk_elems = per * ((chunk + 3) / 4 * 4);
@@ -250,8 +256,10 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
       a.GP = a.KR + (int64_t)N * nbp * KR_REC;
       a.small = h->small;
-      a.AB = (h->cfg.box_u || h->small) ? a.GP + (int64_t)N * nbp * GP_REC : nullptr;
-      a.ABT = (h->cfg.box_u || h->small) ? a.AB + (int64_t)N * nbp * AB_REC : nullptr;
+      a.fwd16 = h->fwd16;
+      T* ab = a.GP + (int64_t)N * nbp * GP_REC;
+      a.AB = (h->cfg.box_u || h->small) ? ab : nullptr;
+      a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;

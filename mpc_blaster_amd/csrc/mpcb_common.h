@@ -18,6 +18,13 @@ struct GroupLds {
 // Per-lane record in the workspace, per stage: 4 gain values (+ box-mode extras).
 template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
 
+// LDS ordering inside a single-wavefront workgroup.  A wave's LDS instructions execute and return
+// in issue order, so a later ds_read sees every earlier ds_write of the same wave with no barrier
+// and no lgkmcnt(0) drain; only the compiler must keep the program order of the LDS accesses,
+// which this (code-free) memory clobber does.  __syncthreads() would drain every outstanding LDS
+// operation at each exchange.  Valid only for 64-thread (one-wave) workgroups.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
+
 // Identity that LLVM cannot see through (keeps selects of array elements as selects).
 template <class T> __device__ __forceinline__ T opq(T x) {
   asm volatile("" : "+v"(x));

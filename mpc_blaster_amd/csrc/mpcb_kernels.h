@@ -30,6 +30,7 @@ struct SolveArgs {
   int box;           // input boxes on
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
+  int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
   T h;               // RK4 step
   T s;               // stage cost scaling
   Model<T> M;
@@ -85,6 +86,7 @@ struct SplitArgs {
   T* PS;             // box path: value-function snapshots for restarts
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
+  int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
@@ -92,6 +94,7 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
                                            hipEvent_t* ev = nullptr);
 template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st);
+template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st);
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance
 template <class T> int64_t solve_slot_elems(int N, int box);
 

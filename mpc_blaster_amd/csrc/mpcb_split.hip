@@ -175,8 +175,9 @@ __device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
   xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
 }
 
-// EXPORT (input-box path): also store column j of [A|B] and the input rows of the stage Hessian
-// for the active-set kernel (a separate instantiation keeps the plain pass's registers lean)
+// EXPORT: code for storing column j of [A|B] (a.AB, a.ABT) and the input rows of the stage
+// Hessian (a.GH) for the 16-lane forward / active-set kernels; each store runs only when its
+// array is set (a separate export-free fp32 instantiation keeps the plain pass's registers lean)
 template <class T, bool EXPORT>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   __shared__ GroupLds<T> lds_all[GROUPS];
@@ -211,7 +212,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   {
     const T xN = soa(a.XU, N, XU_REC, nb, c)[jx * SS];
     L.v[j] = (j < NX) ? xN - xr[(int64_t)N * NX + jx] : T(0);
-    __syncthreads();
+    wave_lds_sync();
     T acc = T(0);
 #pragma unroll
     for (int i = 0; i < NX; ++i) acc += W.QN[jx * NX + i] * L.v[i];
@@ -222,7 +223,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? W.QN[i * NX + jx] : T(0);
-    __syncthreads();
+    wave_lds_sync();
   }
   bool qp_ok = true;
   T kff0 = T(0);
@@ -249,7 +250,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   commit(0);
   T cyb = pyb, cyr = pyr;
   int buf = 0;
-  __syncthreads();
+  wave_lds_sync();
   for (int k = N - 1; k >= 0; --k) {
     if (k > 0) prefetch(k - 1);
     T col[NX];
@@ -264,12 +265,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
       if (EXPORT && a.AB && valid) {
         T* ab = soa(a.AB, k, AB_REC, nb, c);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) ab[(i * NZ + j) * SS] = col[i];
+      }
+      if (EXPORT && a.ABT && valid) {
         T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          ab[(i * NZ + j) * SS] = col[i];
-          abt[(j * NX + i) * SS] = col[i];
-        }
+        for (int i = 0; i < NX; ++i) abt[(j * NX + i) * SS] = col[i];
       }
       T pt = pj;
       if (iterate) {
@@ -282,7 +284,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
     }
-    __syncthreads();
+    wave_lds_sync();
     T hj = T(0);
 #pragma unroll
     for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
@@ -318,7 +320,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       G[i] += w;
       hj += w * L.v[i];
     }
-    if (EXPORT && a.AB && valid && j >= NX) {
+    if (EXPORT && a.GH && valid && j >= NX) {
       T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
@@ -326,9 +328,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
 #pragma unroll
     for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
-    __syncthreads();
+    wave_lds_sync();
     L.hv[j] = hj;
-    __syncthreads();
+    wave_lds_sync();
     T Huu[NU * NU], hu[NU];
 #pragma unroll
     for (int m = 0; m < NU; ++m) {
@@ -369,7 +371,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
         for (int m = 1; m < NU; ++m) kr[(4 * j + m) * SS] = Kj[m];
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_solve.hip).  Every
     // lane publishes its column and takes the entries below its diagonal from the lanes that
     // own them: uniform code instead of per-entry predicated stores.  (L.X is free: this
@@ -378,7 +380,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     for (int i = 0; i < NX; ++i) L.X[j * NX + i] = Pn[i];
     pj = pn;
     if (k > 0) commit(buf ^ 1);
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
     if constexpr (sizeof(T) == 8) {   // the fp64 products read P from LDS
@@ -620,7 +622,7 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     return e != hipSuccess ? e : hipGetLastError();
   }
   if constexpr (sizeof(T) == 4) {
-    if (a.AB) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
+    if (a.ABT) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
     else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
   } else {
     // one fp64 instantiation (export guarded at run time): measured leaner than the export-free
@@ -632,8 +634,10 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
   hipError_t e = hipSuccess;
-  if (a.AB)   // input boxes: active-set iterations over the exported linearisation (mpcb_box.hip)
+  if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_box.hip)
     e = launch_box<T>(a, st);
+  else if (a.fwd && a.fwd16)   // forward pass from the exported [A|B]^T, 16 lanes per instance
+    e = launch_fwd16<T>(a, st);
   else if (a.fwd)
     e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
   if (ev) (void)hipEventRecord(ev[3], st);
