@@ -18,6 +18,8 @@
 // dx_{k+1} = [A_k | B_k] (dx_k, du_k) + gap_k from row j of the cached [A|B].
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/mpcb.h"
 #include "mpcb_kernels.h"
 #include "mpcb_split.h"
@@ -297,44 +299,49 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     const bool write = valid && !done;
     T dxj = T(0);   // state lanes: component jx of dx_k
     if (iterate && j < NX) dxj = a.x0[b * a.x0_sb + jx] - soa(a.XU, 0, XU_REC, nb, c)[jx * SS];
-    // prefetched one stage ahead: own ybar component; input lanes: row ju of the gains (K | k)
-    // and of the stage Hessian (+ h_u); state lanes: row jx of [A|B] and the gap
-    T fyb, fa[NZ + 1], fb[NX + 1];
-    auto fload = [&](int k) {
-      fyb = soa(a.XU, k, XU_REC, nb, c)[j * SS];
+    // prefetched DEPTH stages ahead (two register sets, slots fixed by unrolling by two; one
+    // stage in the register-heavy active-set kernel): own ybar component; input lanes: row ju of
+    // the gains (K | k) and of the stage Hessian (+ h_u); state lanes: row jx of [A|B], the gap
+    constexpr int DEPTH = BOX ? 1 : 2;
+    T fyb[2], fa[2][NZ + 1], fb[2][NX + 1];
+    auto fload = [&](int k, auto sl_tag) {
+      constexpr int sl = decltype(sl_tag)::value;
+      fyb[sl] = soa(a.XU, k, XU_REC, nb, c)[j * SS];
       if (j >= NX) {
         if constexpr (BOX) {
           const T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
 #pragma unroll
-          for (int i = 0; i <= NZ; ++i) fa[i] = gh[i * NU * SS];
+          for (int i = 0; i <= NZ; ++i) fa[sl][i] = gh[i * NU * SS];
         }
         const T* kr = soa(a.KR, k, KR_REC, nb, c);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) fb[i] = kr[(4 * i + ju) * SS];
-        fb[NX] = kr[(4 * NX + ju) * SS];
+        for (int i = 0; i < NX; ++i) fb[sl][i] = kr[(4 * i + ju) * SS];
+        fb[sl][NX] = kr[(4 * NX + ju) * SS];
       } else {
         const T* ab = soa(a.ABT, k, AB_REC, nb, c) + jx * SS;
 #pragma unroll
-        for (int l = 0; l < NZ; ++l) fa[l] = ab[l * NX * SS];
-        fa[NZ] = iterate ? soa(a.GP, k, GP_REC, nb, c)[jx * SS] : T(0);
+        for (int l = 0; l < NZ; ++l) fa[sl][l] = ab[l * NX * SS];
+        fa[sl][NZ] = iterate ? soa(a.GP, k, GP_REC, nb, c)[jx * SS] : T(0);
       }
     };
-    fload(0);
-    for (int k = 0; k < N; ++k) {
+    auto stage = [&](int k, auto sl_tag) {
+      constexpr int sl = decltype(sl_tag)::value;
       T ra[NZ + 1], rb[NX + 1];
 #pragma unroll
-      for (int i = 0; i <= NZ; ++i) ra[i] = fa[i];
+      for (int i = 0; i <= NZ; ++i) ra[i] = fa[sl][i];
 #pragma unroll
-      for (int i = 0; i <= NX; ++i) rb[i] = fb[i];
-      const T yb = fyb;
-      if (k + 1 < N) fload(k + 1);
+      for (int i = 0; i <= NX; ++i) rb[i] = fb[sl][i];
+      const T yb = fyb[sl];
+      if (k + DEPTH < N) fload(k + DEPTH, sl_tag);
       L.v[j] = dxj;   // input lanes overwrite their slot with du below
       wave_lds_sync();
       const bool lo = (sel<NU>(low, ju) >> k) & 1ull, hi = (sel<NU>(up, ju) >> k) & 1ull;
       if (j >= NX) {
-        T du = rb[NX];
+        // four partial sums: the stage's serial chain is these dot products, not their flops
+        T d4[4] = {rb[NX], T(0), T(0), T(0)};
 #pragma unroll
-        for (int i = 0; i < NX; ++i) du += rb[i] * L.v[i];
+        for (int i = 0; i < NX; ++i) d4[i & 3] += rb[i] * L.v[i];
+        const T du = (d4[0] + d4[1]) + (d4[2] + d4[3]);
         // fixed components: the masked recursion set kff = delta and a zero gain row
         dxj = du;
       }
@@ -367,12 +374,20 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         }
       } else {
         if (write && a.X) a.X[(b * (N + 1) + k) * NX + jx] = yb + dxj;
-        T acc = ra[NZ];
+        T a4[4] = {ra[NZ], T(0), T(0), T(0)};
 #pragma unroll
-        for (int l = 0; l < NZ; ++l) acc += ra[l] * z[l];
-        dxj = acc;
+        for (int l = 0; l < NZ; ++l) a4[l & 3] += ra[l] * z[l];
+        dxj = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       }
       wave_lds_sync();
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    fload(0, S0());
+    if (DEPTH == 2 && N > 1) fload(1, S1());
+    for (int k = 0; k < N; k += DEPTH) {
+      stage(k, S0());
+      if (DEPTH == 2 && k + 1 < N) stage(k + 1, S1());
     }
     if (write && a.X && j < NX) a.X[(b * (N + 1) + N) * NX + jx] = soa(a.XU, N, XU_REC, nb, c)[jx * SS] + dxj;
 
