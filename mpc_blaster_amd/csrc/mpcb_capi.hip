@@ -62,6 +62,7 @@ struct mpcb_handle {
   int split;              // 1: three-kernel split path; 0: single-kernel solver (boxes)
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
+  int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -171,6 +172,9 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     int64_t fwd16_max = 16384;
     if (const char* e = getenv("MPCB_FWD16_MAX")) fwd16_max = atoll(e);
     h->fwd16 = (!cfg->box_u && !h->small && chunk <= fwd16_max) ? 1 : 0;
+    int64_t quad_max = 16384;   // the rollout with a lane quad per instance (latency-bound sizes)
+    if (const char* e = getenv("MPCB_QUAD_P1_MAX")) quad_max = atoll(e);
+    h->quad_p1 = (chunk <= quad_max) ? 1 : 0;
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
@@ -257,6 +261,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.GP = a.KR + (int64_t)N * nbp * KR_REC;
       a.small = h->small;
       a.fwd16 = h->fwd16;
+      a.quad_p1 = h->quad_p1;
       T* ab = a.GP + (int64_t)N * nbp * GP_REC;
       a.AB = (h->cfg.box_u || h->small) ? ab : nullptr;
       a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB_REC : nullptr;

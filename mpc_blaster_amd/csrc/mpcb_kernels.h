@@ -31,6 +31,7 @@ struct SolveArgs {
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
+  int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
   T h;               // RK4 step
   T s;               // stage cost scaling
   Model<T> M;
@@ -87,6 +88,7 @@ struct SplitArgs {
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
+  int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.

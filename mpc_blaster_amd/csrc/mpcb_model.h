@@ -201,14 +201,23 @@ namespace mpcb {
 constexpr int LIN_N = 20;      // scalars per RK4 stage
 constexpr int LIN_STAGE = 80;  // per shooting interval (4 stages)
 
-template <class T>
+// sin/cos of the three attitude angles (the default: one thread evaluates all three)
+struct TrigSerial {
+  template <class T>
+  __device__ __forceinline__ void operator()(const T* __restrict__ x, T& sf, T& cf, T& st, T& ct,
+                                             T& sp, T& cp) const {
+    sc(x[3], &sf, &cf);
+    sc(x[4], &st, &ct);
+    sc(x[5], &sp, &cp);
+  }
+};
+
+template <class T, class Trig = TrigSerial>
 __device__ __forceinline__ void f_nom_lin(const T* __restrict__ x, const T* __restrict__ u,
                                           const Model<T>& M, const T w[3], T* __restrict__ f,
-                                          T* __restrict__ c) {
+                                          T* __restrict__ c, const Trig& trig = Trig()) {
   T sf, cf, st, ct, sp, cp;
-  sc(x[3], &sf, &cf);
-  sc(x[4], &st, &ct);
-  sc(x[5], &sp, &cp);
+  trig(x, sf, cf, st, ct, sp, cp);
   const T ict = T(1) / ct;
   const T tt = st * ict;
   const T wx = x[9], wy = x[10], wz = x[11];
@@ -289,26 +298,26 @@ __device__ __forceinline__ void f_tan_lin(const T* __restrict__ c, const T* __re
 }
 
 // Nominal RK4 step that hands each stage's captured scalars to ``sink(stage, c)``.
-template <class T, class Sink>
+template <class T, class Sink, class Trig = TrigSerial>
 __device__ __forceinline__ void rk4_nom(const T* __restrict__ x, const T* __restrict__ u, T h,
                                         const Model<T>& M, const T w[3], T* __restrict__ xn,
-                                        Sink&& sink) {
+                                        Sink&& sink, const Trig& trig = Trig()) {
   constexpr int NX = 12;
   T k[NX], xs[NX], c[LIN_N];
   const T h2 = T(0.5) * h, h6 = h / T(6);
-  f_nom_lin<T>(x, u, M, w, k, c);
+  f_nom_lin<T>(x, u, M, w, k, c, trig);
   sink(0, c);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { xn[i] = k[i]; xs[i] = x[i] + h2 * k[i]; }
-  f_nom_lin<T>(xs, u, M, w, k, c);
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
   sink(1, c);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; xs[i] = x[i] + h2 * k[i]; }
-  f_nom_lin<T>(xs, u, M, w, k, c);
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
   sink(2, c);
 #pragma unroll
   for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; xs[i] = x[i] + h * k[i]; }
-  f_nom_lin<T>(xs, u, M, w, k, c);
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
   sink(3, c);
 #pragma unroll
   for (int i = 0; i < NX; ++i) xn[i] = x[i] + h6 * (xn[i] + k[i]);

@@ -47,28 +47,31 @@ template <class T> __device__ __forceinline__ void copy16(T* dst, const T* src) 
   *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
 }
 
-// Chunks t = lane, lane + 64, ... < 64 * NI of an LDS -> global copy, LDS reads issued in batches
-// of 8 ahead of their stores so the LDS latency is paid once per batch, not once per chunk.
-template <int NI, class Src, class Dst>
+// Chunks t = lane, lane + 64, ... < TOT of an LDS -> global copy, LDS reads issued in batches of
+// 8 ahead of their stores so the LDS latency is paid once per batch, not once per chunk.
+template <int TOT, class Src, class Dst>
 __device__ __forceinline__ void copy_chunks(int lane, Src src, Dst dst) {
+  constexpr int NI = (TOT + 63) / 64;
 #pragma unroll
   for (int g = 0; g < NI; g += 8) {
     u32x4 r[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      if (g + e < NI) r[e] = *reinterpret_cast<const u32x4*>(src((g + e) * 64 + lane));
+      if (g + e < NI && (TOT % 64 == 0 || (g + e) * 64 + lane < TOT))
+        r[e] = *reinterpret_cast<const u32x4*>(src((g + e) * 64 + lane));
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      if (g + e < NI) *reinterpret_cast<u32x4*>(dst((g + e) * 64 + lane)) = r[e];
+      if (g + e < NI && (TOT % 64 == 0 || (g + e) * 64 + lane < TOT))
+        *reinterpret_cast<u32x4*>(dst((g + e) * 64 + lane)) = r[e];
   }
 }
 
 // LDS staging of the wave's 16 quad records of a REC-element stage record; the quad stride
 // REC*4+4 keeps the per-thread writes bank-conflict free (fp32 and fp64).
-template <class T, int REC>
+template <class T, int REC, int NQ = WQ>
 struct QuadStore {
   static constexpr int STRIDE = REC * SS + 4;
-  static constexpr int ELEMS = WQ * STRIDE;
+  static constexpr int ELEMS = NQ * STRIDE;
   T* buf;
   __device__ __forceinline__ void put(int lane, int i, T v) const {
     buf[(lane >> 2) * STRIDE + i * SS + (lane & 3)] = v;
@@ -76,11 +79,10 @@ struct QuadStore {
   // dst = the wave's first quad record (soa(base, k, REC, nb, c0)); nqv quads are valid.  The
   // wave's records are contiguous in the workspace, so chunk t goes to dst + t * V.
   __device__ __forceinline__ void flush(int lane, T* dst, int nqv) const {
-    constexpr int V = 16 / sizeof(T), CPQ = REC * SS / V, TOT = WQ * CPQ;
-    static_assert(TOT % WAVE == 0, "whole wave-instructions");
+    constexpr int V = 16 / sizeof(T), CPQ = REC * SS / V, TOT = NQ * CPQ;
     auto src = [&](int t) { return buf + t * V + (t / CPQ) * 4; };
-    if (nqv == WQ) {
-      copy_chunks<TOT / WAVE>(lane, src, [&](int t) { return dst + t * V; });
+    if (nqv == NQ) {
+      copy_chunks<TOT>(lane, src, [&](int t) { return dst + t * V; });
     } else {
       for (int t = lane; t < nqv * CPQ; t += WAVE) copy16(dst + t * V, src(t));
     }
@@ -172,6 +174,109 @@ __device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
   for (int i = 0; i < NX; ++i) xus.put(lane, i, x[i]);
 #pragma unroll
   for (int m = 0; m < NU; ++m) xus.put(lane, NX + m, T(0));
+  xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
+}
+
+// ---- P1 with a lane quad per instance (small batches) -------------------------------------
+// The rollout's serial chain is dominated by the three sin/cos of every f evaluation.  Here the
+// four lanes of a quad share one instance: lane g < 3 evaluates the sin/cos of angle g and a
+// quad broadcast (DPP quad_perm, no LDS) hands all six values to the four lanes, which then
+// finish f redundantly.  16 instances per one-wave workgroup (4 quads of the workspace layout).
+template <int SRC> __device__ __forceinline__ float qbcast(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), SRC * 0x55, 0xF, 0xF, true));
+}
+template <int SRC> __device__ __forceinline__ double qbcast(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, SRC * 0x55, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), SRC * 0x55, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+struct TrigQuad {
+  int g;   // lane within the quad
+  template <class T>
+  __device__ __forceinline__ void operator()(const T* __restrict__ x, T& sf, T& cf, T& st, T& ct,
+                                             T& sp, T& cp) const {
+    const T ang = sel<3>(x + 3, g);   // bit-tree select: a plain ?: chain becomes scratch
+    T s, c;
+    sc(ang, &s, &c);
+    sf = qbcast<0>(s); cf = qbcast<0>(c);
+    st = qbcast<1>(s); ct = qbcast<1>(c);
+    sp = qbcast<2>(s); cp = qbcast<2>(c);
+  }
+};
+
+constexpr int QI = WAVE / 4;   // instances per workgroup of the quad rollout
+template <class T>
+__device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
+  constexpr int NQ = QI / SS;
+  __shared__ __attribute__((aligned(16))) T lds_cc[QuadStore<T, CCS_REC, NQ>::ELEMS];
+  __shared__ __attribute__((aligned(16))) T lds_xu[QuadStore<T, XU_REC, NQ>::ELEMS];
+  __shared__ __attribute__((aligned(16))) T lds_gp[QuadStore<T, GP_REC, NQ>::ELEMS];
+  const QuadStore<T, CCS_REC, NQ> ccs{lds_cc};
+  const QuadStore<T, XU_REC, NQ> xus{lds_xu};
+  const QuadStore<T, GP_REC, NQ> gps{lds_gp};
+  const int lane = threadIdx.x;
+  const int g = lane & 3;
+  const int ci = lane >> 2;                        // instance within the workgroup
+  const int64_t nb = a.nb;
+  const int64_t c0 = (int64_t)blockIdx.x * QI;
+  const int64_t c = (c0 + ci < nb) ? c0 + ci : nb - 1;
+  const int64_t nq = (nb + SS - 1) / SS;
+  const int nqv = (int)((nq - c0 / SS) < NQ ? nq - c0 / SS : NQ);
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const bool lead = g == 0;                        // the lane that stages the quad's values
+  const TrigQuad trig{g};
+  T w[3] = {T(0), T(0), T(0)};
+  if (a.wind) {
+    w[0] = a.wind[b * a.wind_sb]; w[1] = a.wind[b * a.wind_sb + 1]; w[2] = a.wind[b * a.wind_sb + 2];
+  }
+  const T* xbp = a.xbar + b * (int64_t)(N + 1) * NX;
+  const T* ubp = a.ubar + b * (int64_t)N * NU;
+  const T* ur = a.uref + b * a.uref_sb;
+  T x[NX], u[NU];
+  load_vec<NX>(iterate ? xbp : a.x0 + b * a.x0_sb, x);
+  for (int k = 0; k < N; ++k) {
+    if (iterate) load_vec<NX>(xbp + (int64_t)k * NX, x);
+    load_vec<NU>(iterate ? ubp + (int64_t)k * NU : ur + (int64_t)k * NU, u);
+    if (lead) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) xus.put(ci, i, x[i]);
+#pragma unroll
+      for (int m = 0; m < NU; ++m) xus.put(ci, NX + m, u[m]);
+    }
+    T xn[NX];
+    rk4_nom<T>(x, u, a.h, a.M, w, xn, [&](int stage, const T* cv) {
+      if (lead) {
+#pragma unroll
+        for (int i = 0; i < LIN_N; ++i) ccs.put(ci, stage * LIN_N + i, cv[i]);
+      }
+    }, trig);
+    if (iterate) {
+      const T* nx = xbp + (int64_t)(k + 1) * NX;
+      if (lead) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) gps.put(ci, i, xn[i] - nx[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) x[i] = xn[i];
+    }
+    wave_lds_sync();
+    xus.flush(lane, soa(a.XU, k, XU_REC, nb, c0), nqv);
+    ccs.flush(lane, soa(a.CC, k, CCS_REC, nb, c0), nqv);
+    if (iterate) gps.flush(lane, soa(a.GP, k, GP_REC, nb, c0), nqv);
+    wave_lds_sync();
+  }
+  if (iterate) load_vec<NX>(xbp + (int64_t)N * NX, x);
+  if (lead) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xus.put(ci, i, x[i]);
+#pragma unroll
+    for (int m = 0; m < NU; ++m) xus.put(ci, NX + m, T(0));
+  }
+  wave_lds_sync();
   xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
 }
 
@@ -482,8 +587,8 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
     };
     const bool do_u = a.U && k0 + NS <= N;
     if (nvalid == WAVE) {
-      if (a.X) copy_chunks<NS * CX>(lane, xsrc, xdst);
-      if (do_u) copy_chunks<NS * CU>(lane, usrc, udst);
+      if (a.X) copy_chunks<WAVE * NS * CX>(lane, xsrc, xdst);
+      if (do_u) copy_chunks<WAVE * NS * CU>(lane, usrc, udst);
     } else {
       if (a.X)
         for (int t = lane; t < nvalid * NS * CX; t += WAVE) copy16(xdst(t), xsrc(t));
@@ -584,6 +689,8 @@ template <class T> int64_t split_elems_per_instance(int N, int iterate, int box)
 
 template <class T>
 __global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_wave<T>(a); }
+template <class T>
+__global__ void __launch_bounds__(64) nominal_quad_kernel(SplitArgs<T> a) { nominal_quad<T>(a); }
 template <class T, bool USE_CC>
 __global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
@@ -613,7 +720,10 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
+  if (a.quad_p1)
+    hipLaunchKernelGGL((nominal_quad_kernel<T>), dim3((unsigned)((a.nb + QI - 1) / QI)), dim3(WAVE), 0, st, a);
+  else
+    hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (a.small) {   // linearisation + Riccati + forward over the cached [A|B] (mpcb_box.hip)
     hipError_t e = launch_small<T>(a, st);
