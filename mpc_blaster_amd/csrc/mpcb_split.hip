@@ -31,6 +31,19 @@
 
 namespace mpcb {
 
+#ifdef MPCB_STAMPS
+// Diagnostic build only: per-region cycle counts of the Riccati stage loop of workgroup 0
+// (s_memtime deltas, summed over stages), read back with mpcb_debug_stamps().
+__device__ unsigned long long g_stamps[16];
+#define STAMP_INIT() unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
+#define STAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_prev; st_prev = t_; }
+#define STAMP_DONE() if (blockIdx.x == 0 && threadIdx.x == 0) for (int i_ = 0; i_ < 16; ++i_) g_stamps[i_] = st_acc[i_];
+#else
+#define STAMP_INIT()
+#define STAMP(i)
+#define STAMP_DONE()
+#endif
+
 // ---- wave-staged workspace / output traffic of the thread-per-instance passes (P1, P3) ------
 // P1 and P3 run one thread per instance in single-wave workgroups: 64 instances = 16 quads.  For
 // a fixed stage k the wave's records of any quad-blocked array are ONE contiguous run of
@@ -356,8 +369,10 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   T cyb = pyb, cyr = pyr;
   int buf = 0;
   wave_lds_sync();
+  STAMP_INIT();
   for (int k = N - 1; k >= 0; --k) {
     if (k > 0) prefetch(k - 1);
+    STAMP(0);
     T col[NX];
     {
       const T* cc = &Cst[buf][q][0];
@@ -368,6 +383,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
+      STAMP(1);
       if (EXPORT && a.AB && valid) {
         T* ab = soa(a.AB, k, AB_REC, nb, c);
 #pragma unroll
@@ -390,6 +406,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
     }
     wave_lds_sync();
+    STAMP(2);
     T hj = T(0);
 #pragma unroll
     for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
@@ -402,6 +419,8 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int i = 0; i < NZ; ++i) G[i] = g[i];
     } else {
+      // (measured: v_mfma_f64_16x16x4_f64 for Y and G with an LDS transpose cut this section
+      // from 5.6k to 3.8k cycles per stage but cost more elsewhere, 14.6k vs 13.7k in total)
       T y[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) y[i] = T(0);
@@ -419,6 +438,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
         G[i] = acc;
       }
     }
+    STAMP(3);
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
       const T w = SW[j * NZ + i];
@@ -436,6 +456,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     wave_lds_sync();
     L.hv[j] = hj;
     wave_lds_sync();
+    STAMP(4);
     T Huu[NU * NU], hu[NU];
 #pragma unroll
     for (int m = 0; m < NU; ++m) {
@@ -454,6 +475,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
     for (int m = 0; m < NU; ++m) nh[m] = -G[NX + m];
     chol4_solve(Lc, nh, Kj);
+    STAMP(5);
     T pn = hj;
 #pragma unroll
     for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
@@ -465,6 +487,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
       Pn[i] = acc;
     }
+    STAMP(6);
     kff0 = sel<NU>(kff, ju);
     if (valid) {
       // K[m][j] at 4j + m (state lanes), kff[m] at 4*NX + m (input lanes): the first store is
@@ -477,6 +500,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       }
     }
     wave_lds_sync();
+    STAMP(7);
     // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_solve.hip).  Every
     // lane publishes its column and takes the entries below its diagonal from the lanes that
     // own them: uniform code instead of per-entry predicated stores.  (L.X is free: this
@@ -486,6 +510,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     pj = pn;
     if (k > 0) commit(buf ^ 1);
     wave_lds_sync();
+    STAMP(8);
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
     if constexpr (sizeof(T) == 8) {   // the fp64 products read P from LDS
@@ -497,7 +522,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     buf ^= 1;
     cyb = pyb;
     cyr = pyr;
+    STAMP(9);
   }
+  STAMP_DONE();
   if (valid && j == NX) a.status[b] = qp_ok ? MPCB_STATUS_OK : MPCB_STATUS_QP_FAIL;
   if (valid && !a.fwd && j >= NX) {
     // rollout mode without trajectories: dx_0 = 0 so u0 = ubar_0 + kff_0

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-region cycles of the Riccati stage loop (variant built with -DMPCB_STAMPS).
+
+    MPCB_LIB=mpc_blaster_amd/variants/lib_stamps.so python tools/stamps.py [c2|c3]
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mpc_blaster_amd import BatchedMPC, MPCConfig, _lib  # noqa: E402
+
+w = sys.argv[1] if len(sys.argv) > 1 else 'c2'
+B, dt, ref = (4096, 'f64', 'hover') if w == 'c2' else (65536, 'f32', 'sine')
+N = 20
+m = BatchedMPC(MPCConfig(N=N, dtype=dt), max_batch=B)
+d = m.gen_inputs(B, seed=1002, ref=ref)
+for _ in range(3):
+    m.solve(d['x0'], d['xref'], d['uref'], want_traj=True)
+torch.cuda.synchronize()
+lib = _lib.load()
+out = (ctypes.c_ulonglong * 16)()
+lib.mpcb_debug_stamps.argtypes = [ctypes.c_void_p]
+assert lib.mpcb_debug_stamps(out) == 0
+names = ['prefetch', 'tangent', 'export+Lv/X+sync', 'products', 'stagecost+Hu+syncs', 'chol+solves',
+         'Pn', 'KR store+sync', 'publish+commit+sync', 'Pc select+LP']
+v = np.array(out[:10], dtype=np.float64) / N
+print(f'{w}: cycles per stage (s_memtime units, wave 0):')
+for n, x in zip(names, v):
+    print(f'   {n:24s} {x:9.0f}')
+print(f'   {"total":24s} {v.sum():9.0f}')
