@@ -111,9 +111,15 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       // the input part of ubar (masking), the gap (iterate mode)
       T pcol[NX], pe, pub[NU], pgp[NX];
       auto bload = [&](int k) {
-        const T* ab = soa(a.AB, k, AB_REC, nb, c) + j * SS;
+        const int tv = var_index(j);
+        if (tv >= 0) {
+          const T* ab = soa(a.AB, k, AB_REC, nb, c) + tv * SS;
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pcol[i] = ab[i * NZ * SS];
+          for (int i = 0; i < NX; ++i) pcol[i] = ab[i * NVAR * SS];
+        } else {   // position / velocity directions: e_j, e_j + h e_{j-6}
+#pragma unroll
+          for (int i = 0; i < NX; ++i) pcol[i] = (i == j ? T(1) : T(0)) + ((j >= 6 && i == j - 6) ? a.h : T(0));
+        }
         const T* xu = soa(a.XU, k, XU_REC, nb, c);
         pe = xu[j * SS] - ((j < NX) ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
 #pragma unroll
@@ -320,7 +326,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       } else {
         const T* ab = soa(a.ABT, k, AB_REC, nb, c) + jx * SS;
 #pragma unroll
-        for (int l = 0; l < NZ; ++l) fa[sl][l] = ab[l * NX * SS];
+        for (int t = 0; t < NVAR; ++t) fa[sl][t] = ab[t * NX * SS];
         fa[sl][NZ] = iterate ? soa(a.GP, k, GP_REC, nb, c)[jx * SS] : T(0);
       }
     };
@@ -374,9 +380,11 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         }
       } else {
         if (write && a.X) a.X[(b * (N + 1) + k) * NX + jx] = yb + dxj;
-        T a4[4] = {ra[NZ], T(0), T(0), T(0)};
+        // constant columns: position (identity) and velocity (identity + h into position)
+        const T zc = (jx < 3) ? L.v[jx] + a.h * L.v[jx + 6] : ((jx >= 6 && jx < 9) ? L.v[jx] : T(0));
+        T a4[4] = {ra[NZ], zc, T(0), T(0)};
 #pragma unroll
-        for (int l = 0; l < NZ; ++l) a4[l & 3] += ra[l] * z[l];
+        for (int t = 0; t < NVAR; ++t) a4[(t + 2) & 3] += ra[t] * z[var_col(t)];
         dxj = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       }
       wave_lds_sync();
@@ -489,12 +497,15 @@ __global__ void __launch_bounds__(64) lin_kernel(SplitArgs<T> a) {
   for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
   rk4_tan_g<T, false>([&](int i) { return cc[i * SS + q]; }, dx, du, a.h, a.M, col);
   const int64_t c = q0 * SS + q;
-  T* ab = soa(a.AB, k, AB_REC, nb, c);
-  T* abt = soa(a.ABT, k, AB_REC, nb, c);
+  const int tv = var_index(j);
+  if (tv >= 0) {
+    T* ab = soa(a.AB, k, AB_REC, nb, c);
+    T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    ab[(i * NZ + j) * SS] = col[i];
-    abt[(j * NX + i) * SS] = col[i];
+    for (int i = 0; i < NX; ++i) {
+      ab[(i * NVAR + tv) * SS] = col[i];
+      abt[(tv * NX + i) * SS] = col[i];
+    }
   }
 }
 

@@ -59,13 +59,19 @@ template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipS
 //   GP [N][12][nb]      gap Phi(xbar_k, ubar_k) - xbar_{k+1}      (iterate mode only)
 //   KR [N][52][nb]      K_k (48, K[m][i] at row 4*i+m) | kff_k (4)
 constexpr int XU_REC = 16, CCS_REC = 80, GP_REC = 12, KR_REC = 52;
-// input-box path: column j of [A|B] at j*NX + i; input row m of the stage Hessian (16) + h_u[m]
+// Exported linearisation (16-lane forward pass, active-set kernel).  Only the NVAR columns of
+// [A|B] that depend on the linearisation point are stored: the attitude (3..5), body-rate
+// (9..11) and input (12..15) directions.  The others are constant for this model -- f does not
+// depend on p and v enters only p_dot -- so A e_p = e_p and A e_v = e_v + h e_p exactly.
 // Element orders put the 16 lanes of an instance on CONSECUTIVE elements for every access:
-//   AB  [A|B]_{ij} at i*16 + j (backward: lane j reads column j)
-//   ABT [A|B]_{ij} at j*12 + i (forward: state lane i reads row i)
+//   AB  [A|B]_{i, var_col(t)} at i*NVAR + t (backward: lane j reads its column)
+//   ABT [A|B]_{i, var_col(t)} at t*12 + i   (forward: state lane i reads row i)
 //   GH  input row m of the stage Hessian, entry i (16 = h_u) at i*4 + m
 //   PS  P_k column j entry i (12 = p_k[j]) at i*12 + j
-constexpr int AB_REC = 12 * 16, GH_REC = 4 * 17, PS_REC = 12 * 13;
+constexpr int NVAR = 10;
+__host__ __device__ constexpr int var_col(int t) { return t < 3 ? 3 + t : 6 + t; }
+__host__ __device__ constexpr int var_index(int j) { return (j >= 3 && j < 6) ? j - 3 : (j >= 9 ? j - 6 : -1); }
+constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 
 template <class T>
 struct SplitArgs {

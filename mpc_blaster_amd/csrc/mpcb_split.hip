@@ -384,15 +384,16 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
       STAMP(1);
-      if (EXPORT && a.AB && valid) {
+      const int tv = var_index(j);   // exported: the state-dependent columns only
+      if (EXPORT && a.AB && valid && tv >= 0) {
         T* ab = soa(a.AB, k, AB_REC, nb, c);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) ab[(i * NZ + j) * SS] = col[i];
+        for (int i = 0; i < NX; ++i) ab[(i * NVAR + tv) * SS] = col[i];
       }
-      if (EXPORT && a.ABT && valid) {
+      if (EXPORT && a.ABT && valid && tv >= 0) {
         T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) abt[(j * NX + i) * SS] = col[i];
+        for (int i = 0; i < NX; ++i) abt[(tv * NX + i) * SS] = col[i];
       }
       T pt = pj;
       if (iterate) {
