@@ -459,9 +459,3 @@ extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double 
   return MPCB_OK;
 }
 
-#ifdef MPCB_STAMPS
-namespace mpcb { extern __device__ unsigned long long g_stamps[16]; }
-extern "C" int mpcb_debug_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
-}
-#endif

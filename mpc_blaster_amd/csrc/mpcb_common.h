@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mpcb_kernels.h"
 
 namespace mpcb {
@@ -24,6 +26,14 @@ template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
 // which this (code-free) memory clobber does.  __syncthreads() would drain every outstanding LDS
 // operation at each exchange.  Valid only for 64-thread (one-wave) workgroups.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
+
+// f(std::integral_constant<int, i>{}) for i = 0 .. n-1 (compile-time lane indices for DPP)
+template <int n, class F, int i = 0> __device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (i < n) {
+    f(std::integral_constant<int, i>{});
+    static_for<n, F, i + 1>(static_cast<F&&>(f));
+  }
+}
 
 // Identity that LLVM cannot see through (keeps selects of array elements as selects).
 template <class T> __device__ __forceinline__ T opq(T x) {

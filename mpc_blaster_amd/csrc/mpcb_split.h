@@ -51,6 +51,62 @@ __device__ __forceinline__ v16f outer12(const float a[12], const float b[12]) {
   return acc;
 }
 
+// ---- fp64 row-broadcast FMAs (gfx950 DPP64: v_fmac_f64_dpp ... row_newbcast:L) -------------
+// Lane L of every 16-lane row (= one instance of the Riccati layout) broadcasts its src0 to the
+// whole row inside the FMA itself, so the fp64 block contractions read their operands from the
+// owning lanes' registers instead of LDS (the LDS products were bound by the CU's LDS bandwidth:
+// every lane read all of P and [A|B] each stage).  One asm block per broadcast pattern; the
+// leading s_nop covers the VALU-write -> DPP-read and EXEC-write -> DPP wait states that the
+// compiler's hazard recognizer does not insert for inline asm (DPP sources are never written
+// inside a block).
+#define MPCB_BC(d, s, b, l) \
+  "v_fmac_f64_dpp %" #d ", %" #s ", %" #b " row_newbcast:" l " row_mask:0xf bank_mask:0xf\n\t"
+
+// acc[i] += bcast_L(a[i]) * b  (i < 12) and acc12 += bcast_L(a12) * b
+template <int L>
+__device__ __forceinline__ void fmac13_bc(double (&acc)[12], double& acc12, const double (&a)[12],
+                                          double a12, double b) {
+  asm("s_nop 4\n\t"
+      MPCB_BC(0, 13, 26, "%c27") MPCB_BC(1, 14, 26, "%c27") MPCB_BC(2, 15, 26, "%c27")
+      MPCB_BC(3, 16, 26, "%c27") MPCB_BC(4, 17, 26, "%c27") MPCB_BC(5, 18, 26, "%c27")
+      MPCB_BC(6, 19, 26, "%c27") MPCB_BC(7, 20, 26, "%c27") MPCB_BC(8, 21, 26, "%c27")
+      MPCB_BC(9, 22, 26, "%c27") MPCB_BC(10, 23, 26, "%c27") MPCB_BC(11, 24, 26, "%c27")
+      MPCB_BC(12, 25, 26, "%c27")
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+        "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11]),
+        "+v"(acc12)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+        "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a12), "v"(b), "i"(L));
+}
+
+// acc[i] += bcast_i(a) * b  (i < 16): lane i's a feeds accumulator i
+__device__ __forceinline__ void fmac16_diag(double (&acc)[16], double a, double b) {
+  asm("s_nop 4\n\t"
+      MPCB_BC(0, 16, 17, "0") MPCB_BC(1, 16, 17, "1") MPCB_BC(2, 16, 17, "2")
+      MPCB_BC(3, 16, 17, "3") MPCB_BC(4, 16, 17, "4") MPCB_BC(5, 16, 17, "5")
+      MPCB_BC(6, 16, 17, "6") MPCB_BC(7, 16, 17, "7") MPCB_BC(8, 16, 17, "8")
+      MPCB_BC(9, 16, 17, "9") MPCB_BC(10, 16, 17, "10") MPCB_BC(11, 16, 17, "11")
+      MPCB_BC(12, 16, 17, "12") MPCB_BC(13, 16, 17, "13") MPCB_BC(14, 16, 17, "14")
+      MPCB_BC(15, 16, 17, "15")
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+        "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11]),
+        "+v"(acc[12]), "+v"(acc[13]), "+v"(acc[14]), "+v"(acc[15])
+      : "v"(a), "v"(b));
+}
+
+// acc[i] += bcast_i(a) * b  (i < 12)
+__device__ __forceinline__ void fmac12_diag(double (&acc)[12], double a, double b) {
+  asm("s_nop 4\n\t"
+      MPCB_BC(0, 12, 13, "0") MPCB_BC(1, 12, 13, "1") MPCB_BC(2, 12, 13, "2")
+      MPCB_BC(3, 12, 13, "3") MPCB_BC(4, 12, 13, "4") MPCB_BC(5, 12, 13, "5")
+      MPCB_BC(6, 12, 13, "6") MPCB_BC(7, 12, 13, "7") MPCB_BC(8, 12, 13, "8")
+      MPCB_BC(9, 12, 13, "9") MPCB_BC(10, 12, 13, "10") MPCB_BC(11, 12, 13, "11")
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+        "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11])
+      : "v"(a), "v"(b));
+}
+#undef MPCB_BC
+
 // Quad-blocked SoA chunk layouts: instances are grouped in quads (the 4 instances of one P2
 // wavefront); element i of the stage-k record of chunk instance c lives at
 //   base[((k * nquad + c / 4) * REC + i) * 4 + c % 4],   element stride SS = 4.

@@ -21,6 +21,11 @@
 #include "mpcb_common.h"
 #include "mpcb_split.h"
 
+// fp64 Riccati products through DPP row broadcasts (1) or LDS operands (0, the earlier path)
+#ifndef MPCB_P2_DPP
+#define MPCB_P2_DPP 1
+#endif
+
 #ifndef MPCB_P2_WAVES
 #define MPCB_P2_WAVES
 #endif
@@ -402,16 +407,32 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       }
       L.hv[j] = pt;
     }
-    if constexpr (sizeof(T) == 8) {   // fp64 path contracts through LDS; fp32 uses MFMA
+    if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // LDS-operand fp64 products
 #pragma unroll
       for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
     }
     wave_lds_sync();
     STAMP(2);
     T hj = T(0);
+    T G[NZ];
+    if constexpr (sizeof(T) == 8 && MPCB_P2_DPP) {
+      // Y = P [A|B], h = [A|B]^T pt and G = [A|B]^T Y with row-broadcast FMAs: lane l supplies
+      // column l of P (= row l) and pt_l, lane i supplies column i of [A|B]; no LDS operands
+      double y[NX], g[NZ];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) y[i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) g[i] = 0.0;
+      const double ptl = L.hv[j];
+      static_for<NX>([&](auto l) { fmac13_bc<decltype(l)::value>(y, hj, Pc, ptl, col[l]); });
+#pragma unroll
+      for (int l = 0; l < NX; ++l) fmac16_diag(g, col[l], y[l]);
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) G[i] = g[i];
+    } else {
 #pragma unroll
     for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
-    T G[NZ];
+    }
     if constexpr (sizeof(T) == 4) {
       // Y = P [A|B] and G = [A|B]^T Y on the matrix cores (24 MFMAs per 4 instances)
       float y[16], g[16];
@@ -419,7 +440,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       to_columns(outer12(col, y), g);      // lane (q,j): G_q[:, j]
 #pragma unroll
       for (int i = 0; i < NZ; ++i) G[i] = g[i];
-    } else {
+    } else if constexpr (!MPCB_P2_DPP) {
       // (measured: v_mfma_f64_16x16x4_f64 for Y and G with an LDS transpose cut this section
       // from 5.6k to 3.8k cycles per stage but cost more elsewhere, 14.6k vs 13.7k in total)
       T y[NX];
@@ -481,12 +502,20 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
     for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
     T Pn[NX];
+    if constexpr (sizeof(T) == 8 && MPCB_P2_DPP) {
+      // Pn[i] = G[i] + sum_m H_ux[m][i] K[m][j]: lane i owns H_ux[:, i] = its G[NX..]
 #pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      T acc = G[i];
+      for (int i = 0; i < NX; ++i) Pn[i] = G[i];
 #pragma unroll
-      for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
-      Pn[i] = acc;
+      for (int m = 0; m < NU; ++m) fmac12_diag(Pn, G[NX + m], Kj[m]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        T acc = G[i];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
+        Pn[i] = acc;
+      }
     }
     STAMP(6);
     kff0 = sel<NU>(kff, ju);
@@ -514,7 +543,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(8);
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
-    if constexpr (sizeof(T) == 8) {   // the fp64 products read P from LDS
+    if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // the LDS fp64 products read P from LDS
       if (j < NX) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) L.P[j * NX + i] = Pc[i];
@@ -788,3 +817,10 @@ template int64_t split_elems_per_instance<double>(int, int, int);
 template int64_t split_elems_per_instance<float>(int, int, int);
 
 }  // namespace mpcb
+
+#ifdef MPCB_STAMPS
+// (same translation unit as g_stamps: the library is built without -fgpu-rdc)
+extern "C" int mpcb_debug_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+}
+#endif
