@@ -59,20 +59,30 @@ template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
   return (j & 8) ? opq(l2[1]) : opq(l2[0]);
 }
 
+// 1 / sqrt(x): fp32 sqrt + IEEE reciprocal; fp64 from the hardware estimate v_rsq_f64 refined
+// by two Newton steps (~1 ulp, a fraction of the instructions of sqrt + an IEEE division).
+// A non-positive pivot still yields NaN/inf, which the callers' status checks catch.
+__device__ __forceinline__ float inv_sqrt(float x) { return 1.0f / sqrtf(x); }
+__device__ __forceinline__ double inv_sqrt(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double e = fma(-x * r, r, 1.0);   // 1 - x r^2
+    r = fma(0.5 * r, e, r);
+  }
+  return r;
+}
+
 template <class T>
 __device__ __forceinline__ void chol4(const T H[16], T L[10]) {
   // L packed lower: L00 L10 L11 L20 L21 L22 L30 L31 L32 L33 (diagonal holds 1/L_ii)
-  T l00 = sqrt(H[0]);
-  T i00 = T(1) / l00;
+  T i00 = inv_sqrt(H[0]);
   T l10 = H[4] * i00, l20 = H[8] * i00, l30 = H[12] * i00;
-  T l11 = sqrt(H[5] - l10 * l10);
-  T i11 = T(1) / l11;
+  T i11 = inv_sqrt(H[5] - l10 * l10);
   T l21 = (H[9] - l20 * l10) * i11, l31 = (H[13] - l30 * l10) * i11;
-  T l22 = sqrt(H[10] - l20 * l20 - l21 * l21);
-  T i22 = T(1) / l22;
+  T i22 = inv_sqrt(H[10] - l20 * l20 - l21 * l21);
   T l32 = (H[14] - l30 * l20 - l31 * l21) * i22;
-  T l33 = sqrt(H[15] - l30 * l30 - l31 * l31 - l32 * l32);
-  T i33 = T(1) / l33;
+  T i33 = inv_sqrt(H[15] - l30 * l30 - l31 * l31 - l32 * l32);
   L[0] = i00; L[1] = l10; L[2] = i11; L[3] = l20; L[4] = l21; L[5] = i22;
   L[6] = l30; L[7] = l31; L[8] = l32; L[9] = i33;
 }
