@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MPCB_ABI_VERSION 1
+#define MPCB_ABI_VERSION 2
 
 enum { MPCB_F64 = 0, MPCB_F32 = 1 };
 enum { MPCB_MODE_ROLLOUT = 0, MPCB_MODE_ITERATE = 1 };
@@ -52,8 +52,8 @@ enum { MPCB_STATUS_OK = 0, MPCB_STATUS_NAN = 1, MPCB_STATUS_MAXITER = 2, MPCB_ST
  * Matrices are row-major, leading dimension nx (Q, QN) or nu (R).
  */
 typedef struct mpcb_config {
-  int32_t nx;            /* 12 (rigid-body slice); 17 reserved for the full model */
-  int32_t nu;            /* 4 */
+  int32_t nx;            /* 12 (rigid-body slice, the BASELINE configs) or 17 (full model) */
+  int32_t nu;            /* 4 or 6 */
   int32_t N;             /* horizon (ocp.dims.N, blastermodel.py:226) */
   int32_t dtype;         /* MPCB_F64 | MPCB_F32 */
   int32_t box_u;         /* 1: lbu <= u <= ubu on stages 0..N-1 (idxbu, blastermodel.py:261) */
@@ -61,7 +61,7 @@ typedef struct mpcb_config {
   int32_t reserved[2];
   double dt;             /* Tf / N (solver_options.tf, blastermodel.py:287) */
   double cost_scale;     /* stage-cost scaling; acados uses time_steps[k] = dt */
-  double mass, lx, ly, c, g, t_blast;
+  double mass, lx, ly, c, g, t_blast;   /* 17/6: t_blast is the default parameter p[24] */
   double J[9];           /* inertia (row-major 3x3) */
   double Q[MPCB_MAX_NX * MPCB_MAX_NX];   /* stage state weight  (W[:nx,:nx]) */
   double R[MPCB_MAX_NU * MPCB_MAX_NU];   /* stage input weight  (W[nx:,nx:]) */
@@ -149,6 +149,16 @@ int mpcb_sim_step(mpcb_handle* h, int64_t B, const void* x, const void* u, const
 int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_t id_offset, int ref_kind,
                     void* x0, void* xref, int64_t xref_sb, void* uref, int64_t uref_sb,
                     void* wind, void* hip_stream);
+
+/*
+ * Model parameters of the full 17/6 model (nx == 17): acados ``ocp_solver.set(k, 'p', p)`` /
+ * ``integrator.set('p', p)`` (simulation_blaster.py:69, blastermodel.py:203-210), the same
+ * vector on every stage.  ``params`` is a DEVICE array [B|1, 25] (column-major vec of
+ * J_angles 3x2, J_euler 3x3, J_p 3x3, then T_blast) that the caller keeps alive for the later
+ * solve / linearize / sim_step calls; stride 0 broadcasts; NULL restores the defaults
+ * (zeros, T_blast = cfg.t_blast).  MPCB_E_UNSUPPORTED on a 12/4 handle.
+ */
+int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb);
 
 /* Histogram of u0 per input channel over [lo, hi) into counts[nu][nbins] (int64, accumulated). */
 int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,

@@ -19,7 +19,7 @@ STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram', 'mpcb_set_timing',
-           'mpcb_last_timing')
+           'mpcb_last_timing', 'mpcb_set_params')
 
 
 class MpcbConfig(ctypes.Structure):
@@ -77,6 +77,7 @@ def load(path: str | None = None):
     lib.mpcb_histogram.argtypes = [vp, i64, vp, dbl, dbl, i32, vp, vp]
     lib.mpcb_set_timing.argtypes = [vp, i32]
     lib.mpcb_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    lib.mpcb_set_params.argtypes = [vp, vp, i64]
     for name in EXPORTS:
         if name not in ('mpcb_last_error', 'mpcb_workspace_bytes'):
             getattr(lib, name).restype = i32

@@ -13,7 +13,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .config import NU, NX, MPCConfig
+from .config import MPCConfig
 
 
 def _torch():
@@ -39,7 +39,9 @@ class BatchedMPC:
                                             ctypes.byref(h)))
         self._h = h
         self.dtype = config.torch_dtype
+        self.nx, self.nu = config.nx, config.nu
         self._u0 = self._X = self._U = self._status = None
+        self._params = None
 
     # ------------------------------------------------------------------ helpers
     def close(self):
@@ -96,11 +98,11 @@ class BatchedMPC:
         torch = _torch()
         dev = f'cuda:{self.device}'
         N = self.cfg.N
-        self._u0 = torch.empty((B, NU), dtype=self.dtype, device=dev)
+        self._u0 = torch.empty((B, self.nu), dtype=self.dtype, device=dev)
         self._status = torch.empty((B,), dtype=torch.int32, device=dev)
         if want_traj:
-            self._X = torch.empty((B, N + 1, NX), dtype=self.dtype, device=dev)
-            self._U = torch.empty((B, N, NU), dtype=self.dtype, device=dev)
+            self._X = torch.empty((B, N + 1, self.nx), dtype=self.dtype, device=dev)
+            self._U = torch.empty((B, N, self.nu), dtype=self.dtype, device=dev)
         else:
             self._X = self._U = None
 
@@ -116,12 +118,12 @@ class BatchedMPC:
         Returns the first-step controls u0* [B,4] (device tensor, async).
         """
         N = self.cfg.N
-        x0, _ = self._dev(x0, (NX,), 'x0')
+        x0, _ = self._dev(x0, (self.nx,), 'x0')
         B = x0.shape[0]
         if B > self.max_batch:
             raise ValueError(f'batch {B} > max_batch {self.max_batch}')
-        xr, xr_sb = self._dev(x_ref, (N + 1, NX), 'x_ref', B, allow_broadcast=True)
-        ur, ur_sb = self._dev(u_ref, (N, NU), 'u_ref', B, allow_broadcast=True)
+        xr, xr_sb = self._dev(x_ref, (N + 1, self.nx), 'x_ref', B, allow_broadcast=True)
+        ur, ur_sb = self._dev(u_ref, (N, self.nu), 'u_ref', B, allow_broadcast=True)
         wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
         if out is None:
             self._outputs(B, want_traj)
@@ -129,7 +131,7 @@ class BatchedMPC:
             self._u0, self._X, self._U, self._status = out
         self._keep = (x0, xr, ur, wd)
         _lib.check(self.lib.mpcb_solve(
-            self._h, B, self._ptr(x0), NX, self._ptr(xr), xr_sb, self._ptr(ur), ur_sb,
+            self._h, B, self._ptr(x0), self.nx, self._ptr(xr), xr_sb, self._ptr(ur), ur_sb,
             self._ptr(wd), wd_sb, self._ptr(self._u0), self._ptr(self._X), self._ptr(self._U),
             self._ptr(self._status), self._stream()))
         return self._u0
@@ -137,12 +139,12 @@ class BatchedMPC:
     def solve_iterate(self, x0, xbar, ubar, x_ref, u_ref, wind=None, out=None):
         """acados SQP_RTI step from the persistent iterate (xbar [B,N+1,12], ubar [B,N,4])."""
         N = self.cfg.N
-        x0, _ = self._dev(x0, (NX,), 'x0')
+        x0, _ = self._dev(x0, (self.nx,), 'x0')
         B = x0.shape[0]
-        xb, _ = self._dev(xbar, (N + 1, NX), 'xbar', B)
-        ub, _ = self._dev(ubar, (N, NU), 'ubar', B)
-        xr, xr_sb = self._dev(x_ref, (N + 1, NX), 'x_ref', B, allow_broadcast=True)
-        ur, ur_sb = self._dev(u_ref, (N, NU), 'u_ref', B, allow_broadcast=True)
+        xb, _ = self._dev(xbar, (N + 1, self.nx), 'xbar', B)
+        ub, _ = self._dev(ubar, (N, self.nu), 'ubar', B)
+        xr, xr_sb = self._dev(x_ref, (N + 1, self.nx), 'x_ref', B, allow_broadcast=True)
+        ur, ur_sb = self._dev(u_ref, (N, self.nu), 'u_ref', B, allow_broadcast=True)
         wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
         if out is None:
             self._outputs(B, True)
@@ -150,10 +152,22 @@ class BatchedMPC:
             self._u0, self._X, self._U, self._status = out
         self._keep = (x0, xb, ub, xr, ur, wd)
         _lib.check(self.lib.mpcb_solve_iterate(
-            self._h, B, self._ptr(x0), NX, self._ptr(xb), self._ptr(ub), self._ptr(xr), xr_sb,
+            self._h, B, self._ptr(x0), self.nx, self._ptr(xb), self._ptr(ub), self._ptr(xr), xr_sb,
             self._ptr(ur), ur_sb, self._ptr(wd), wd_sb, self._ptr(self._u0), self._ptr(self._X),
             self._ptr(self._U), self._ptr(self._status), self._stream()))
         return self._u0
+
+    def set_params(self, p):
+        """Parameters of the full 17/6 model, [B|1, 25] (acados ``set(k, 'p', p)``,
+        simulation_blaster.py:69): column-major J_angles 3x2, J_euler 3x3, J_p 3x3, T_blast.
+        ``None`` restores the defaults (zeros, T_blast = config.t_blast)."""
+        if p is None:
+            self._params = None
+            _lib.check(self.lib.mpcb_set_params(self._h, ctypes.c_void_p(0), 0))
+            return
+        t, sb = self._dev(p, (25,), 'p')
+        self._params = t   # the library keeps the device pointer: hold the tensor
+        _lib.check(self.lib.mpcb_set_params(self._h, self._ptr(t), 0 if t.shape[0] == 1 else 25))
 
     def get_control(self):
         """First-step control u0* of the last solve, [B,4] device tensor."""
@@ -179,14 +193,14 @@ class BatchedMPC:
         """A [B,N,12,12], B [B,N,12,4], Phi(xbar_k, ubar_k) [B,N,12] (debug / parity)."""
         torch = _torch()
         N = self.cfg.N
-        xb, _ = self._dev(xbar, (N + 1, NX), 'xbar')
+        xb, _ = self._dev(xbar, (N + 1, self.nx), 'xbar')
         B = xb.shape[0]
-        ub, _ = self._dev(ubar, (N, NU), 'ubar', B)
+        ub, _ = self._dev(ubar, (N, self.nu), 'ubar', B)
         wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
         dev = f'cuda:{self.device}'
-        A = torch.empty((B, N, NX, NX), dtype=self.dtype, device=dev)
-        Bm = torch.empty((B, N, NX, NU), dtype=self.dtype, device=dev)
-        xn = torch.empty((B, N, NX), dtype=self.dtype, device=dev)
+        A = torch.empty((B, N, self.nx, self.nx), dtype=self.dtype, device=dev)
+        Bm = torch.empty((B, N, self.nx, self.nu), dtype=self.dtype, device=dev)
+        xn = torch.empty((B, N, self.nx), dtype=self.dtype, device=dev)
         _lib.check(self.lib.mpcb_linearize(self._h, B, self._ptr(xb), self._ptr(ub), self._ptr(wd),
                                            wd_sb, self._ptr(A), self._ptr(Bm), self._ptr(xn),
                                            self._stream()))
@@ -196,9 +210,9 @@ class BatchedMPC:
     def sim_step(self, x, u, T=None, wind=None):
         """Plant integrator: one RK4 step of length T (default dt) — AcadosSimSolver.solve()."""
         torch = _torch()
-        xs, _ = self._dev(x, (NX,), 'x')
+        xs, _ = self._dev(x, (self.nx,), 'x')
         B = xs.shape[0]
-        us, _ = self._dev(u, (NU,), 'u', B)
+        us, _ = self._dev(u, (self.nu,), 'u', B)
         wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
         xo = torch.empty_like(xs)
         _lib.check(self.lib.mpcb_sim_step(self._h, B, self._ptr(xs), self._ptr(us), self._ptr(wd),
@@ -212,14 +226,14 @@ class BatchedMPC:
         torch = _torch()
         N = self.cfg.N
         dev = f'cuda:{self.device}'
-        x0 = torch.empty((B, NX), dtype=self.dtype, device=dev)
+        x0 = torch.empty((B, self.nx), dtype=self.dtype, device=dev)
         if ref == 'sine':
-            xr = torch.empty((B, N + 1, NX), dtype=self.dtype, device=dev)
-            xr_sb, kind = (N + 1) * NX, 1
+            xr = torch.empty((B, N + 1, self.nx), dtype=self.dtype, device=dev)
+            xr_sb, kind = (N + 1) * self.nx, 1
         else:
-            xr = torch.empty((1, N + 1, NX), dtype=self.dtype, device=dev)
+            xr = torch.empty((1, N + 1, self.nx), dtype=self.dtype, device=dev)
             xr_sb, kind = 0, 0
-        ur = torch.empty((1, N, NU), dtype=self.dtype, device=dev)
+        ur = torch.empty((1, N, self.nu), dtype=self.dtype, device=dev)
         wd = torch.empty((B, 3), dtype=self.dtype, device=dev) if wind else None
         _lib.check(self.lib.mpcb_gen_inputs(self._h, B, int(seed), int(id_offset), kind,
                                             self._ptr(x0), self._ptr(xr), xr_sb, self._ptr(ur), 0,
@@ -229,9 +243,9 @@ class BatchedMPC:
     def histogram(self, u0, lo=0.0, hi=65.0, nbins=64, counts=None):
         """Accumulate a per-motor histogram of u0 into int64 counts [4, nbins] (device)."""
         torch = _torch()
-        u, _ = self._dev(u0, (NU,), 'u0')
+        u, _ = self._dev(u0, (self.nu,), 'u0')
         if counts is None:
-            counts = torch.zeros((NU, nbins), dtype=torch.int64, device=f'cuda:{self.device}')
+            counts = torch.zeros((self.nu, nbins), dtype=torch.int64, device=f'cuda:{self.device}')
         _lib.check(self.lib.mpcb_histogram(self._h, u.shape[0], self._ptr(u), float(lo), float(hi),
                                            int(nbins), self._ptr(counts), self._stream()))
         return counts

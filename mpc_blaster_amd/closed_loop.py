@@ -8,17 +8,17 @@ plant integrator (AcadosSimSolver: one RK4 step of Tsim = Tf/N, JSON ``Tsim``) a
 from __future__ import annotations
 
 from .api import BatchedMPC
-from .config import NU, NX
 
 
 def closed_loop(mpc: BatchedMPC, x0, x_ref, u_ref, nsim: int, wind=None, plant_T=None,
                 xbar=None, ubar=None):
-    """Returns (X_sim [B, nsim+1, 12], U_sim [B, nsim, 4], status [B] = max over steps)."""
+    """Returns (X_sim [B, nsim+1, nx], U_sim [B, nsim, nu], status [B] = max over steps)."""
     import torch
     dev = f'cuda:{mpc.device}'
     dt = mpc.dtype
     x = torch.as_tensor(x0, dtype=dt, device=dev).contiguous()
     B, N = x.shape[0], mpc.cfg.N
+    NX, NU = mpc.nx, mpc.nu
     xb = torch.zeros((B, N + 1, NX), dtype=dt, device=dev) if xbar is None else \
         torch.as_tensor(xbar, dtype=dt, device=dev).clone()
     ub = torch.zeros((B, N, NU), dtype=dt, device=dev) if ubar is None else \

@@ -16,19 +16,26 @@ import numpy as np
 
 from . import _lib
 
-NX, NU = 12, 4
+NX, NU = 12, 4          # the rigid-body slice (BASELINE configs)
+NX17, NU17 = 17, 6      # the full reference model
 
 
-def _default_Q():
-    return np.diag([1e3] * 6 + [5.0] * 3 + [10.0] * 3)
+def _default_Q(nx=NX):
+    # simulation_blaster.py:24 (JSON cost.W diag[0:17]); the 12/4 slice keeps the first 12
+    q = [1e3] * 6 + [5.0] * 3 + [10.0] * 3 + [1e-2] * 2 + [1e3] * 3
+    return np.diag(q[:nx])
 
 
-def _default_R():
-    return np.diag([0.05] * 4)
+def _default_R(nu=NU):
+    # simulation_blaster.py:27 (JSON cost.W diag[17:23])
+    r = [0.05] * 4 + [1e-5] * 2
+    return np.diag(r[:nu])
 
 
 @dataclass
 class MPCConfig:
+    """nx/nu select the model: 12/4 (the rigid-body slice, BASELINE configs, MI355X-tuned
+    kernels) or 17/6 (the full reference model; ``MPCConfig.full()`` gives the JSON-pinned OCP)."""
     N: int = 20
     dt: float = 1.0 / 30.0
     dtype: str = 'f64'                 # 'f64' | 'f32'
@@ -39,25 +46,39 @@ class MPCConfig:
     c: float = 0.03
     g: float = 9.81
     t_blast: float = 0.0
-    Q: np.ndarray = field(default_factory=_default_Q)
-    R: np.ndarray = field(default_factory=_default_R)
+    Q: np.ndarray | None = None        # default diag of simulation_blaster.py:24
+    R: np.ndarray | None = None        # default diag of simulation_blaster.py:27
     QN: np.ndarray | None = None       # default 10 * Q
     cost_scale: float | None = None    # default dt
     lbu: np.ndarray | None = None      # None -> no input box
     ubu: np.ndarray | None = None
     max_as_iter: int = 200
+    nx: int = NX
+    nu: int = NU
 
     def __post_init__(self):
-        self.Q = np.asarray(self.Q, dtype=np.float64)
-        self.R = np.asarray(self.R, dtype=np.float64)
+        if (self.nx, self.nu) not in ((NX, NU), (NX17, NU17)):
+            raise ValueError(f'nx/nu {self.nx}/{self.nu}: the models are 12/4 and 17/6')
+        self.Q = _default_Q(self.nx) if self.Q is None else np.asarray(self.Q, dtype=np.float64)
+        self.R = _default_R(self.nu) if self.R is None else np.asarray(self.R, dtype=np.float64)
         self.QN = 10.0 * self.Q if self.QN is None else np.asarray(self.QN, dtype=np.float64)
         self.J = np.asarray(self.J, dtype=np.float64)
-        if self.Q.shape != (NX, NX) or self.QN.shape != (NX, NX) or self.R.shape != (NU, NU):
-            raise ValueError('Q/QN must be 12x12 and R 4x4 for the 12-state/4-input model')
+        nx, nu = self.nx, self.nu
+        if self.Q.shape != (nx, nx) or self.QN.shape != (nx, nx) or self.R.shape != (nu, nu):
+            raise ValueError(f'Q/QN must be {nx}x{nx} and R {nu}x{nu} for the {nx}/{nu} model')
         if self.dtype not in ('f64', 'f32'):
             raise ValueError(f'dtype {self.dtype!r}')
         if (self.lbu is None) != (self.ubu is None):
             raise ValueError('lbu and ubu must be given together')
+
+    @classmethod
+    def full(cls, **kw) -> 'MPCConfig':
+        """The reference's own OCP (acados_ocp_blasterModel.json, simulation_blaster.py:12-30):
+        17/6 model, N = 60, Tf = 2 (dt = 1/30), T_blast = 2.2 * 9.81, W = diag(Q17, R6),
+        W_e = 10 Q17.  Input/state boxes are not applied."""
+        d = dict(N=60, dt=2.0 / 60.0, t_blast=2.2 * 9.81, nx=NX17, nu=NU17)
+        d.update(kw)
+        return cls(**d)
 
     @property
     def boxed(self) -> bool:
@@ -69,7 +90,7 @@ class MPCConfig:
 
     def to_c(self) -> _lib.MpcbConfig:
         c = _lib.MpcbConfig()
-        c.nx, c.nu, c.N = NX, NU, int(self.N)
+        c.nx, c.nu, c.N = int(self.nx), int(self.nu), int(self.N)
         c.dtype = _lib.MPCB_F64 if self.dtype == 'f64' else _lib.MPCB_F32
         c.box_u = 1 if self.boxed else 0
         c.max_as_iter = int(self.max_as_iter)
@@ -86,9 +107,9 @@ class MPCConfig:
         for i, v in enumerate(self.R.reshape(-1)):
             c.R[i] = float(v)
         if self.boxed:
-            lb = np.broadcast_to(np.asarray(self.lbu, dtype=np.float64), (NU,))
-            ub = np.broadcast_to(np.asarray(self.ubu, dtype=np.float64), (NU,))
-            for i in range(NU):
+            lb = np.broadcast_to(np.asarray(self.lbu, dtype=np.float64), (self.nu,))
+            ub = np.broadcast_to(np.asarray(self.ubu, dtype=np.float64), (self.nu,))
+            for i in range(self.nu):
                 c.lbu[i], c.ubu[i] = float(lb[i]), float(ub[i])
         return c
 

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../../include/mpcb.h"
+#include "mpcb_full.h"
 #include "mpcb_kernels.h"
 
 using namespace mpcb;
@@ -74,6 +75,11 @@ struct mpcb_handle {
   int timed_chunks = 0;   // chunks recorded by the last solve (0: nothing recorded)
   int timed_split = 0;
   hipEvent_t ev[TCHUNKS][4] = {};
+  // full 17/6 model (cfg.nx == 17): per-instance parameters set by mpcb_set_params (nullable:
+  // the defaults in the weights block), chunk of instances per launch
+  int full = 0;
+  const void* params = nullptr;
+  int64_t params_sb = 0;
 };
 
 extern "C" const char* mpcb_last_error(void) { return g_err.c_str(); }
@@ -96,6 +102,22 @@ static void fill_weights(const mpcb_config& c, Weights<T>& w) {
 }
 
 template <class T>
+static void fill_weights17(const mpcb_config& c, Weights17<T>& w) {
+  for (int i = 0; i < NX17 * NX17; ++i) {
+    w.Q[i] = (T)c.Q[i];
+    w.QN[i] = (T)c.QN[i];
+  }
+  for (int i = 0; i < NU17 * NU17; ++i) w.R[i] = (T)c.R[i];
+  for (int i = 0; i < NU17; ++i) {
+    w.lbu[i] = (T)c.lbu[i];
+    w.ubu[i] = (T)c.ubu[i];
+  }
+  // acados parameter_values default: every Jacobian block 0, T_blast from the config
+  for (int i = 0; i < NP17; ++i) w.p[i] = T(0);
+  w.p[24] = (T)c.t_blast;
+}
+
+template <class T>
 static void fill_model(const mpcb_config& c, const double* Jinv, Model<T>& M) {
   M.minv = (T)(1.0 / c.mass);
   M.g = (T)c.g;
@@ -112,9 +134,12 @@ static void fill_model(const mpcb_config& c, const double* Jinv, Model<T>& M) {
 extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
   if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");
   *out = nullptr;
-  if (cfg->nx != NX || cfg->nu != NU)
-    return fail(MPCB_E_UNSUPPORTED, "nx=%d nu=%d: this build implements the 12-state/4-input model",
+  const bool full = cfg->nx == NX17 && cfg->nu == NU17;
+  if (!(cfg->nx == NX && cfg->nu == NU) && !full)
+    return fail(MPCB_E_UNSUPPORTED, "nx=%d nu=%d: implemented models are 12/4 (rigid-body slice) and 17/6 (full)",
                 cfg->nx, cfg->nu);
+  if (full && cfg->box_u)
+    return fail(MPCB_E_UNSUPPORTED, "input boxes are implemented for the 12/4 model only");
   if (cfg->N < 1 || cfg->N > 4096) return fail(MPCB_E_INVALID, "horizon N=%d out of range", cfg->N);
   if (cfg->box_u && cfg->N > 64) return fail(MPCB_E_UNSUPPORTED, "box_u needs N <= 64 (N=%d)", cfg->N);
   if (cfg->dtype != MPCB_F64 && cfg->dtype != MPCB_F32)
@@ -145,12 +170,25 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   // Path: the split kernels win at every measured batch size (c2: 4096); the single-kernel
   // solver (mpcb_solve.hip) serves the input-box active-set loop and, on request
   // (MPCB_SPLIT_MIN_BATCH above the batch), small unconstrained batches.
+  if (full) {
+    // one chunk of instances per launch triple; ~N*516 scalars of workspace each
+    int64_t chunk = 8192;
+    if (const char* e = getenv("MPCB_CHUNK")) chunk = atoll(e);
+    if (chunk < 64) chunk = 64;
+    if (chunk > max_batch) chunk = max_batch;
+    h->full = 1;
+    h->split = 1;
+    h->chunk = chunk;
+    h->chunk_elems = full17_elems(cfg->N) * chunk;
+    h->scratch_bytes = h->chunk_elems * (int64_t)esz;
+  }
   int64_t split_min = 1;
   if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
-  h->split = (max_batch >= split_min) ? 1 : 0;
+  if (!full) h->split = (max_batch >= split_min) ? 1 : 0;
   if (const char* e = getenv("MPCB_BOX_IMPL"))   // "v1": the single-kernel active-set solver
     if (cfg->box_u && strcmp(e, "v1") == 0) h->split = 0;
-  if (!h->split) {
+  if (full) {
+  } else if (!h->split) {
     h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
     h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
   } else {
@@ -188,14 +226,23 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     delete h;
     return fail(MPCB_E_NOMEM, "workspace %lld bytes: %s", (long long)h->scratch_bytes, hipGetErrorString(e));
   }
-  const size_t wbytes = f64 ? sizeof(Weights<double>) : sizeof(Weights<float>);
+  const size_t wbytes = full ? (f64 ? sizeof(Weights17<double>) : sizeof(Weights17<float>))
+                             : (f64 ? sizeof(Weights<double>) : sizeof(Weights<float>));
   e = hipMalloc(&h->weights, wbytes);
   if (e != hipSuccess) {
     (void)hipFree(h->scratch);
     delete h;
     return fail(MPCB_E_NOMEM, "weights: %s", hipGetErrorString(e));
   }
-  if (f64) {
+  if (full && f64) {
+    Weights17<double> w;
+    fill_weights17(*cfg, w);
+    e = hipMemcpy(h->weights, &w, sizeof(w), hipMemcpyHostToDevice);
+  } else if (full) {
+    Weights17<float> w;
+    fill_weights17(*cfg, w);
+    e = hipMemcpy(h->weights, &w, sizeof(w), hipMemcpyHostToDevice);
+  } else if (f64) {
     Weights<double> w;
     fill_weights(*cfg, w);
     e = hipMemcpy(h->weights, &w, sizeof(w), hipMemcpyHostToDevice);
@@ -231,6 +278,31 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
                       const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
                       const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                       void* u0, void* X, void* U, int32_t* status, void* stream) {
+  if (h->full) {
+    if (wind) return fail(MPCB_E_UNSUPPORTED, "wind is a 12/4-model extension");
+    FullArgs<T> a;
+    a.N = h->cfg.N;
+    a.mode = mode;
+    a.h = (T)h->cfg.dt;
+    a.s = (T)h->cfg.cost_scale;
+    if constexpr (sizeof(T) == 8) a.M = h->Md; else a.M = h->Mf;
+    a.W = reinterpret_cast<const Weights17<T>*>(h->weights);
+    a.p = (const T*)h->params; a.p_sb = h->params_sb;
+    a.x0 = (const T*)x0; a.x0_sb = x0_sb;
+    a.xref = (const T*)xref; a.xref_sb = xref_sb;
+    a.uref = (const T*)uref; a.uref_sb = uref_sb;
+    a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
+    a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
+    a.ws = (T*)h->scratch;
+    for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
+      a.b0 = b0;
+      a.nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
+      hipError_t e = launch_full17<T>(a, (hipStream_t)stream);
+      if (e != hipSuccess) return fail(MPCB_E_HIP, "full17 launch: %s", hipGetErrorString(e));
+    }
+    h->timed_chunks = 0;   // per-phase timing is implemented for the 12/4 kernels
+    return MPCB_OK;
+  }
   if (h->split) {
     SplitArgs<T> a;
     a.N = h->cfg.N;
@@ -389,7 +461,21 @@ extern "C" int mpcb_linearize(mpcb_handle* h, int64_t B, const void* xbar, const
   if (!xbar || !ubar || !A || !Bm || !xnext) return fail(MPCB_E_INVALID, "null array");
   HIP_TRY(hipSetDevice(h->device));
   hipError_t e;
-  if (h->cfg.dtype == MPCB_F64)
+  if (h->full) {
+    if (wind) return fail(MPCB_E_UNSUPPORTED, "wind is a 12/4-model extension");
+    const int64_t psb = h->params ? h->params_sb : 0;
+    if (h->cfg.dtype == MPCB_F64) {
+      const double* p = h->params ? (const double*)h->params : reinterpret_cast<const Weights17<double>*>(h->weights)->p;
+      e = launch_linearize17<double>(B, h->cfg.N, h->cfg.dt, h->Md, p, psb, (const double*)xbar,
+                                     (const double*)ubar, (double*)A, (double*)Bm, (double*)xnext,
+                                     (hipStream_t)stream);
+    } else {
+      const float* p = h->params ? (const float*)h->params : reinterpret_cast<const Weights17<float>*>(h->weights)->p;
+      e = launch_linearize17<float>(B, h->cfg.N, (float)h->cfg.dt, h->Mf, p, psb, (const float*)xbar,
+                                    (const float*)ubar, (float*)A, (float*)Bm, (float*)xnext,
+                                    (hipStream_t)stream);
+    }
+  } else if (h->cfg.dtype == MPCB_F64)
     e = launch_linearize<double>(B, h->cfg.N, h->cfg.dt, h->Md, (const double*)xbar, (const double*)ubar,
                                  (const double*)wind, wind_sb, (double*)A, (double*)Bm, (double*)xnext,
                                  (hipStream_t)stream);
@@ -410,7 +496,19 @@ extern "C" int mpcb_sim_step(mpcb_handle* h, int64_t B, const void* x, const voi
   if (!(T > 0)) return fail(MPCB_E_INVALID, "T must be > 0");
   HIP_TRY(hipSetDevice(h->device));
   hipError_t e;
-  if (h->cfg.dtype == MPCB_F64)
+  if (h->full) {
+    if (wind) return fail(MPCB_E_UNSUPPORTED, "wind is a 12/4-model extension");
+    const int64_t psb = h->params ? h->params_sb : 0;
+    if (h->cfg.dtype == MPCB_F64) {
+      const double* p = h->params ? (const double*)h->params : reinterpret_cast<const Weights17<double>*>(h->weights)->p;
+      e = launch_sim_step17<double>(B, T, h->Md, p, psb, (const double*)x, (const double*)u,
+                                    (double*)x_out, (hipStream_t)stream);
+    } else {
+      const float* p = h->params ? (const float*)h->params : reinterpret_cast<const Weights17<float>*>(h->weights)->p;
+      e = launch_sim_step17<float>(B, (float)T, h->Mf, p, psb, (const float*)x, (const float*)u,
+                                   (float*)x_out, (hipStream_t)stream);
+    }
+  } else if (h->cfg.dtype == MPCB_F64)
     e = launch_sim_step<double>(B, T, h->Md, (const double*)x, (const double*)u, (const double*)wind,
                                 wind_sb, (double*)x_out, (hipStream_t)stream);
   else
@@ -427,6 +525,7 @@ extern "C" int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_
   if (B == 0) return MPCB_OK;
   if (!x0 || !xref || !uref) return fail(MPCB_E_INVALID, "null array");
   if (ref_kind == 1 && xref_sb == 0) return fail(MPCB_E_INVALID, "sinusoid refs need xref_sb > 0");
+  if (h->full) return fail(MPCB_E_UNSUPPORTED, "the synthetic generator covers the 12/4 configs");
   HIP_TRY(hipSetDevice(h->device));
   hipError_t e;
   if (h->cfg.dtype == MPCB_F64)
@@ -445,6 +544,7 @@ extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double 
                    int64_t* counts, void* stream) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
   if (B < 0 || nbins < 1 || nbins > 4096 || !(hi > lo)) return fail(MPCB_E_INVALID, "bad histogram args");
+  if (h->full) return fail(MPCB_E_UNSUPPORTED, "the u0 histogram covers the 12/4 configs");
   if (B == 0) return MPCB_OK;
   if (!u0 || !counts) return fail(MPCB_E_INVALID, "null array");
   HIP_TRY(hipSetDevice(h->device));
@@ -459,3 +559,11 @@ extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double 
   return MPCB_OK;
 }
 
+extern "C" int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (!h->full) return fail(MPCB_E_UNSUPPORTED, "the 12/4 model takes T_blast from the config");
+  if (params_sb < 0) return fail(MPCB_E_INVALID, "negative parameter stride");
+  h->params = params;
+  h->params_sb = params ? params_sb : 0;
+  return MPCB_OK;
+}

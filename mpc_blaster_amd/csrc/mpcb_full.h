@@ -1,0 +1,226 @@
+// mpcb_full.h — the full 17-state / 6-input BLASTER model on the device.
+//
+// Restates f_expl_expr of src/scripts/blastermodel.py:70-201 with every state and parameter:
+//   x = [p(3), eta = (phi, theta, psi), v(3), omega(3), alpha(2), poc(3)]      (:171-190)
+//   u = [T0..T3, alpha1_dot, alpha2_dot]                                       (:191-193)
+//   p = vec(J_angles 3x2) | vec(J_euler 3x3) | vec(J_p 3x3) | T_blast (column-major, :203-210)
+//   p_dot     = v
+//   eta_dot   = inv(R_to_omega(phi, theta)) omega                              (:128-141, :162)
+//   v_dot     = R (e3 sum T + R_gimbal e3 T_blast) / m - g e3                   (:143-163)
+//               R = Rz Ry Rx (:103-122), R_gimbal e3 = Ry(a1) Rx(a2) e3 = [s1 c2, -s2, c1 c2]
+//   omega_dot = inv(J) (M(T) - omega x J omega)                                (:95-101, :164)
+//   alpha_dot = u[4:6]
+//   poc_dot   = J_p v + J_euler eta_dot + J_angles alpha_dot                   (:165-167)
+// ``f17_tan`` evaluates f and one directional derivative J_f (dx, du) in the same pass
+// (forward-mode dual numbers: each lane of an instance seeds one of the 23 directions).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mpcb_model.h"
+
+namespace mpcb {
+
+constexpr int NX17 = 17, NU17 = 6, NZ17 = NX17 + NU17, NP17 = 25;
+
+// per-instance parameters unpacked from the 25-vector (row-major blocks)
+template <class T>
+struct P17 {
+  T Ja[6];   // J_angles 3x2
+  T Je[9];   // J_euler  3x3
+  T Jp[9];   // J_p      3x3
+  T tb;      // T_blast
+};
+
+template <class T>
+__device__ __forceinline__ void unpack_p17(const T* __restrict__ p, P17<T>& P) {
+  // column-major vec (blastermodel.py:203-210): block[i][j] = p[off + j*3 + i]
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) P.Ja[i * 2 + j] = p[j * 3 + i];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      P.Je[i * 3 + j] = p[6 + j * 3 + i];
+      P.Jp[i * 3 + j] = p[15 + j * 3 + i];
+    }
+  }
+  P.tb = p[24];
+}
+
+template <class T, bool TAN>
+__device__ __forceinline__ void f17_tan(const T* __restrict__ x, const T* __restrict__ dx,
+                                        const T* __restrict__ u, const T* __restrict__ du,
+                                        const Model<T>& M, const P17<T>& P, T* __restrict__ f,
+                                        T* __restrict__ df) {
+  T sf, cf, st, ct, sp, cp, s1, c1, s2, c2;
+  sc(x[3], &sf, &cf);
+  sc(x[4], &st, &ct);
+  sc(x[5], &sp, &cp);
+  sc(x[12], &s1, &c1);
+  sc(x[13], &s2, &c2);
+  const T ict = T(1) / ct;
+  const T tt = st * ict;
+  const T wx = x[9], wy = x[10], wz = x[11];
+  f[0] = x[6]; f[1] = x[7]; f[2] = x[8];
+  const T a = sf * wy + cf * wz;
+  const T b = cf * wy - sf * wz;
+  const T ed0 = wx + tt * a, ed1 = b, ed2 = a * ict;
+  f[3] = ed0; f[4] = ed1; f[5] = ed2;
+  // R = Rz(psi) Ry(theta) Rx(phi)
+  const T cpst = cp * st, spst = sp * st;
+  const T R00 = cp * ct, R01 = cpst * sf - sp * cf, R02 = cpst * cf + sp * sf;
+  const T R10 = sp * ct, R11 = spst * sf + cp * cf, R12 = spst * cf - cp * sf;
+  const T R20 = -st, R21 = ct * sf, R22 = ct * cf;
+  // body force: motors along e3 plus the swivelled blaster thrust
+  const T Tsum = (u[0] + u[1]) + (u[2] + u[3]);
+  const T fb0 = P.tb * (s1 * c2), fb1 = -P.tb * s2, fb2 = Tsum + P.tb * (c1 * c2);
+  f[6] = (R00 * fb0 + R01 * fb1 + R02 * fb2) * M.minv;
+  f[7] = (R10 * fb0 + R11 * fb1 + R12 * fb2) * M.minv;
+  f[8] = (R20 * fb0 + R21 * fb1 + R22 * fb2) * M.minv - M.g;
+  const T jw0 = M.J[0] * wx + M.J[1] * wy + M.J[2] * wz;
+  const T jw1 = M.J[3] * wx + M.J[4] * wy + M.J[5] * wz;
+  const T jw2 = M.J[6] * wx + M.J[7] * wy + M.J[8] * wz;
+  const T k0 = wy * jw2 - wz * jw1;
+  const T k1 = wz * jw0 - wx * jw2;
+  const T k2 = wx * jw1 - wy * jw0;
+  const T m0 = (u[1] + u[3] - u[0] - u[2]) * M.ly - k0;
+  const T m1 = (u[1] + u[2] - u[0] - u[3]) * M.lx - k1;
+  const T m2 = (u[2] + u[3] - u[0] - u[1]) * M.c - k2;
+  f[9] = M.Jinv[0] * m0 + M.Jinv[1] * m1 + M.Jinv[2] * m2;
+  f[10] = M.Jinv[3] * m0 + M.Jinv[4] * m1 + M.Jinv[5] * m2;
+  f[11] = M.Jinv[6] * m0 + M.Jinv[7] * m1 + M.Jinv[8] * m2;
+  f[12] = u[4];
+  f[13] = u[5];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    f[14 + i] = P.Jp[i * 3] * x[6] + P.Jp[i * 3 + 1] * x[7] + P.Jp[i * 3 + 2] * x[8] +
+                P.Je[i * 3] * ed0 + P.Je[i * 3 + 1] * ed1 + P.Je[i * 3 + 2] * ed2 +
+                P.Ja[i * 2] * u[4] + P.Ja[i * 2 + 1] * u[5];
+  if constexpr (TAN) {
+    const T dphi = dx[3], dth = dx[4], dpsi = dx[5];
+    const T dwx = dx[9], dwy = dx[10], dwz = dx[11];
+    const T dsf = cf * dphi, dcf = -sf * dphi;
+    const T dst = ct * dth, dct = -st * dth;
+    const T dsp = cp * dpsi, dcp = -sp * dpsi;
+    const T ds1 = c1 * dx[12], dc1 = -s1 * dx[12];
+    const T ds2 = c2 * dx[13], dc2 = -s2 * dx[13];
+    const T dict = -ict * ict * dct;
+    const T dtt = dst * ict + st * dict;
+    df[0] = dx[6]; df[1] = dx[7]; df[2] = dx[8];
+    const T da = dsf * wy + sf * dwy + dcf * wz + cf * dwz;
+    const T db = dcf * wy + cf * dwy - dsf * wz - sf * dwz;
+    const T ded0 = dwx + dtt * a + tt * da, ded1 = db, ded2 = da * ict + a * dict;
+    df[3] = ded0; df[4] = ded1; df[5] = ded2;
+    const T dcpst = dcp * st + cp * dst, dspst = dsp * st + sp * dst;
+    const T dR00 = dcp * ct + cp * dct;
+    const T dR01 = dcpst * sf + cpst * dsf - dsp * cf - sp * dcf;
+    const T dR02 = dcpst * cf + cpst * dcf + dsp * sf + sp * dsf;
+    const T dR10 = dsp * ct + sp * dct;
+    const T dR11 = dspst * sf + spst * dsf + dcp * cf + cp * dcf;
+    const T dR12 = dspst * cf + spst * dcf - dcp * sf - cp * dsf;
+    const T dR20 = -dst, dR21 = dct * sf + ct * dsf, dR22 = dct * cf + ct * dcf;
+    const T dTsum = (du[0] + du[1]) + (du[2] + du[3]);
+    const T dfb0 = P.tb * (ds1 * c2 + s1 * dc2), dfb1 = -P.tb * ds2;
+    const T dfb2 = dTsum + P.tb * (dc1 * c2 + c1 * dc2);
+    df[6] = (dR00 * fb0 + dR01 * fb1 + dR02 * fb2 + R00 * dfb0 + R01 * dfb1 + R02 * dfb2) * M.minv;
+    df[7] = (dR10 * fb0 + dR11 * fb1 + dR12 * fb2 + R10 * dfb0 + R11 * dfb1 + R12 * dfb2) * M.minv;
+    df[8] = (dR20 * fb0 + dR21 * fb1 + dR22 * fb2 + R20 * dfb0 + R21 * dfb1 + R22 * dfb2) * M.minv;
+    const T djw0 = M.J[0] * dwx + M.J[1] * dwy + M.J[2] * dwz;
+    const T djw1 = M.J[3] * dwx + M.J[4] * dwy + M.J[5] * dwz;
+    const T djw2 = M.J[6] * dwx + M.J[7] * dwy + M.J[8] * dwz;
+    const T dk0 = dwy * jw2 + wy * djw2 - dwz * jw1 - wz * djw1;
+    const T dk1 = dwz * jw0 + wz * djw0 - dwx * jw2 - wx * djw2;
+    const T dk2 = dwx * jw1 + wx * djw1 - dwy * jw0 - wy * djw0;
+    const T dm0 = (du[1] + du[3] - du[0] - du[2]) * M.ly - dk0;
+    const T dm1 = (du[1] + du[2] - du[0] - du[3]) * M.lx - dk1;
+    const T dm2 = (du[2] + du[3] - du[0] - du[1]) * M.c - dk2;
+    df[9] = M.Jinv[0] * dm0 + M.Jinv[1] * dm1 + M.Jinv[2] * dm2;
+    df[10] = M.Jinv[3] * dm0 + M.Jinv[4] * dm1 + M.Jinv[5] * dm2;
+    df[11] = M.Jinv[6] * dm0 + M.Jinv[7] * dm1 + M.Jinv[8] * dm2;
+    df[12] = du[4];
+    df[13] = du[5];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      df[14 + i] = P.Jp[i * 3] * dx[6] + P.Jp[i * 3 + 1] * dx[7] + P.Jp[i * 3 + 2] * dx[8] +
+                   P.Je[i * 3] * ded0 + P.Je[i * 3 + 1] * ded1 + P.Je[i * 3 + 2] * ded2 +
+                   P.Ja[i * 2] * du[4] + P.Ja[i * 2 + 1] * du[5];
+  }
+}
+
+// One classic RK4 step (acados sim_erk: 4 stages, 1 step) of f17 with an optional tangent.
+template <class T, bool TAN>
+__device__ __forceinline__ void rk4_17(const T* __restrict__ x, const T* __restrict__ dx,
+                                       const T* __restrict__ u, const T* __restrict__ du, T h,
+                                       const Model<T>& M, const P17<T>& P, T* __restrict__ xn,
+                                       T* __restrict__ dxn) {
+  T k[NX17], dk[NX17], xs[NX17], dxs[NX17];
+  const T h2 = T(0.5) * h, h6 = h / T(6);
+  f17_tan<T, TAN>(x, dx, u, du, M, P, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    xn[i] = k[i];
+    xs[i] = x[i] + h2 * k[i];
+    if constexpr (TAN) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  }
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    xn[i] += T(2) * k[i];
+    xs[i] = x[i] + h2 * k[i];
+    if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
+  }
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    xn[i] += T(2) * k[i];
+    xs[i] = x[i] + h * k[i];
+    if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
+  }
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    xn[i] = x[i] + h6 * (xn[i] + k[i]);
+    if constexpr (TAN) dxn[i] = dx[i] + h6 * (dxn[i] + dk[i]);
+  }
+}
+
+// Device-resident weights of the 17/6 OCP (row-major) and the default parameter vector.
+template <class T>
+struct Weights17 {
+  T Q[NX17 * NX17];
+  T R[NU17 * NU17];
+  T QN[NX17 * NX17];
+  T lbu[NU17], ubu[NU17];
+  T p[NP17];
+};
+
+template <class T>
+struct FullArgs {
+  int64_t b0, nb;    // first global instance of the chunk, instances in the chunk
+  int N, mode;
+  T h, s;
+  Model<T> M;
+  const Weights17<T>* W;
+  const T* p; int64_t p_sb;   // parameters [B|1, 25]; nullptr -> W->p
+  const T* x0; int64_t x0_sb;
+  const T* xref; int64_t xref_sb;
+  const T* uref; int64_t uref_sb;
+  const T* xbar; const T* ubar;
+  T* u0; T* X; T* U; int32_t* status;
+  T* ws;             // chunk workspace: per instance full17_elems(N) elements
+};
+
+__host__ __device__ constexpr int64_t full17_elems(int N) {
+  // XB (N+1)x17 | UB Nx6 | AB N x 23 columns x 17 | KR N x (6x17 + 6) | GP N x 17
+  return (int64_t)(N + 1) * NX17 + (int64_t)N * (NU17 + NZ17 * NX17 + NU17 * NX17 + NU17 + NX17);
+}
+
+template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st);
+template <class T>
+hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
+                              const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st);
+template <class T>
+hipError_t launch_sim_step17(int64_t B, T h, const Model<T>& M, const T* p, int64_t p_sb,
+                             const T* x, const T* u, T* xo, hipStream_t st);
+
+}  // namespace mpcb

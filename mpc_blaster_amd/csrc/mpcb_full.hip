@@ -1,0 +1,449 @@
+// mpcb_full.hip — one SQP_RTI step of the reference's full 17-state / 6-input OCP
+// (blastermodel.py:70-292, acados_ocp_blasterModel.json: N = 60, Tf = 2,
+// W = diag(Q17, R6), W_e = 10 Q17, 25 parameters).
+//
+// Three launches per chunk:
+//   nominal17  one thread per instance: the RK4 rollout of u_ref from x0 (or a copy of the
+//              persistent iterate) into the workspace;
+//   lin17ws    stage-parallel linearisation, 32 lanes per (instance, stage): lane j < 23
+//              integrates the RK4 tangent seeded with e_j, so column j of [A_k | B_k] lands in
+//              lane j (what acados' forward VDE computes); gaps in iterate mode;
+//   riccati17  32 lanes per instance (two per one-wave workgroup), lane j owning column j of the
+//              stage Hessian: the Riccati recursion over the cached [A|B] (P, [A|B] and the
+//              Hessian columns meet in LDS, the 6x6 input block is factorised redundantly per
+//              lane, P is symmetric by construction), then the forward pass (du = K dx + k on the
+//              input lanes, dx' = [A|B] (dx, du) + gap on the state lanes, exchanged through
+//              LDS) writing u0, X = xbar + dx, U = ubar + du and the status.
+// The 12/4 slice has its own MI355X-tuned kernels (mpcb_split.hip); this path carries the full
+// model at the reference's own dimensions and is not on the BASELINE benchmark configs.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcb.h"
+#include "mpcb_common.h"
+#include "mpcb_full.h"
+
+namespace mpcb {
+
+constexpr int L17 = 32;            // lanes per instance
+constexpr int G17 = 64 / L17;      // instances per wavefront
+
+template <class T>
+struct FullLds {
+  T P[NX17 * NX17];   // P[l*17 + i] = column l of P_{k+1}
+  T X[L17 * NX17];    // X[j*17 + i] = [A|B]_{i j}; reused for P's symmetric exchange
+  T Hu[L17 * NU17];   // Hu[j*6 + m] = G_{17+m, j}
+  T v[L17];           // e = ybar - yref (own component per lane)
+  T hv[L17];          // p + P b, then the gradient h
+  T z[L17];           // forward pass exchange (dx | du)
+  T gp[NX17];         // gap of this stage
+};
+
+// n x n Cholesky (row-major H, lower L with 1/L_ii on the diagonal) and the solve L L^T x = b
+template <class T, int n>
+__device__ __forceinline__ void chol_n(const T* __restrict__ H, T* __restrict__ L) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      T acc = H[i * n + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) acc -= L[i * n + k] * L[j * n + k];
+      if (i == j) L[i * n + i] = inv_sqrt(acc);
+      else L[i * n + j] = acc * L[j * n + j];
+    }
+  }
+}
+template <class T, int n>
+__device__ __forceinline__ void chol_n_solve(const T* __restrict__ L, const T* __restrict__ b,
+                                             T* __restrict__ x) {
+  T y[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    T acc = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) acc -= L[i * n + k] * y[k];
+    y[i] = acc * L[i * n + i];
+  }
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i) {
+    T acc = y[i];
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) acc -= L[k * n + i] * x[k];
+    x[i] = acc * L[i * n + i];
+  }
+}
+
+// x[i] for a lane-dependent i < 17 without dynamic register indexing
+template <class T> __device__ __forceinline__ T sel17(const T* x, int i) {
+  const T lo = sel<16>(x, i & 15);
+  return (i == 16) ? x[16] : lo;
+}
+
+// Per-instance workspace carve (FullArgs::ws, full17_elems(N) elements per instance).
+template <class T>
+struct Ws17 {
+  T *XB, *UB, *AB, *KR, *GP;
+  static constexpr int KR_N = NU17 * NX17 + NU17;
+  __device__ __forceinline__ Ws17(T* ws, int N) {
+    XB = ws;                                     // [N+1][17] nominal states
+    UB = XB + (int64_t)(N + 1) * NX17;           // [N][6]    nominal inputs
+    AB = UB + (int64_t)N * NU17;                 // [N][23][17] column j of [A_k|B_k] at j*17
+    KR = AB + (int64_t)N * NZ17 * NX17;          // [N][6*17 + 6]: K[m][i] at i*6 + m, then k
+    GP = KR + (int64_t)N * KR_N;                 // [N][17] gaps
+  }
+};
+
+// ---- phase 0: nominal trajectory, one thread per instance (a serial RK4 chain) ---------------
+template <class T>
+__global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
+  const int64_t c = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (c >= a.nb) return;
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  Ws17<T> w(a.ws + c * full17_elems(N), N);
+  if (iterate) {   // the persistent iterate (X/U may alias xbar/ubar: copy it first)
+    for (int i = 0; i < (N + 1) * NX17; ++i) w.XB[i] = a.xbar[b * (int64_t)(N + 1) * NX17 + i];
+    for (int i = 0; i < N * NU17; ++i) w.UB[i] = a.ubar[b * (int64_t)N * NU17 + i];
+    return;
+  }
+  P17<T> P;
+  unpack_p17(a.p ? a.p + b * a.p_sb : a.W->p, P);
+  const T* ur = a.uref + b * a.uref_sb;
+  T x[NX17], u[NU17];
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    x[i] = a.x0[b * a.x0_sb + i];
+    w.XB[i] = x[i];
+  }
+  for (int k = 0; k < N; ++k) {
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) {
+      u[m] = ur[(int64_t)k * NU17 + m];
+      w.UB[(int64_t)k * NU17 + m] = u[m];
+    }
+    T xn[NX17];
+    rk4_17<T, false>(x, nullptr, u, nullptr, a.h, a.M, P, xn, nullptr);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      x[i] = xn[i];
+      w.XB[(int64_t)(k + 1) * NX17 + i] = xn[i];
+    }
+  }
+}
+
+// ---- the linearisation of every interval, stage-parallel: 32 lanes per (instance, stage) -----
+// Lane j < 23 integrates the RK4 tangent seeded with e_j: column j of [A_k | B_k] (acados'
+// forward VDE).  LIN_WS: into the workspace (+ gaps, iterate mode); else into dense A / Bm.
+template <class T, bool LIN_WS>
+__device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>& M, const T* p,
+                                           int64_t p_sb, const T* xbar, const T* ubar, int64_t b0,
+                                           T* ws, int mode, T* A, T* Bm, T* xnext) {
+  const int lane = threadIdx.x;
+  const int j = lane % L17;
+  const int64_t idx = (int64_t)blockIdx.x * G17 + lane / L17;   // (instance, stage) pair
+  if (idx >= B * N || j >= NZ17) return;
+  const int64_t c = idx / N;
+  const int k = (int)(idx % N);
+  const int64_t b = b0 + c;
+  P17<T> P;
+  unpack_p17(p + b * p_sb, P);
+  const T* xk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)k * NX17 : xbar + (b * (N + 1) + k) * NX17;
+  const T* uk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)(N + 1) * NX17 + (int64_t)k * NU17
+                       : ubar + (b * N + k) * NU17;
+  T x[NX17], u[NU17], dx[NX17], du[NU17], xn[NX17], col[NX17];
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    x[i] = xk[i];
+    dx[i] = (j == i) ? T(1) : T(0);
+  }
+#pragma unroll
+  for (int m = 0; m < NU17; ++m) {
+    u[m] = uk[m];
+    du[m] = (j == NX17 + m) ? T(1) : T(0);
+  }
+  rk4_17<T, true>(x, dx, u, du, h, M, P, xn, col);
+  if constexpr (LIN_WS) {
+    Ws17<T> w(ws + c * full17_elems(N), N);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) w.AB[((int64_t)k * NZ17 + j) * NX17 + i] = col[i];
+    if (j == 0) {   // gap Phi(xbar_k, ubar_k) - xbar_{k+1}; the rollout is gap-free by construction
+#pragma unroll
+      for (int i = 0; i < NX17; ++i)
+        w.GP[(int64_t)k * NX17 + i] = (mode == MPCB_MODE_ITERATE) ? xn[i] - xk[NX17 + i] : T(0);
+    }
+  } else {
+    const int64_t o = b * N + k;
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      if (j < NX17) A[(o * NX17 + i) * NX17 + j] = col[i];
+      else Bm[(o * NX17 + i) * NU17 + (j - NX17)] = col[i];
+    }
+    if (j == 0 && xnext) {
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) xnext[o * NX17 + i] = xn[i];
+    }
+  }
+}
+
+template <class T>
+__global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
+  lin17_body<T, true>(a.nb, a.N, a.h, a.M, a.p ? a.p : a.W->p, a.p ? a.p_sb : 0, nullptr, nullptr,
+                      a.b0, a.ws, a.mode, nullptr, nullptr, nullptr);
+}
+
+// ---- phases 1 + 2: Riccati backward over the cached [A|B], then the forward pass -------------
+template <class T>
+__global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
+  __shared__ FullLds<T> lds_all[G17];
+  __shared__ T SW[NZ17 * NZ17];   // s * blkdiag(Q, R)
+  const int lane = threadIdx.x;
+  const int q = lane / L17;
+  const int j = lane % L17;
+  const bool dir = j < NZ17;                   // lane owns a direction
+  const int jd = dir ? j : 0;
+  const int jx = j < NX17 ? j : 0;
+  const int ju = (j >= NX17 && j < NZ17) ? j - NX17 : 0;
+  FullLds<T>& L = lds_all[q];
+  const int64_t c_raw = (int64_t)blockIdx.x * G17 + q;
+  const bool valid = c_raw < a.nb;
+  const int64_t c = valid ? c_raw : a.nb - 1;  // a ragged last wave shadows the last instance
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const T s = a.s;
+  const Weights17<T>& W = *a.W;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const T* xr = a.xref + b * a.xref_sb;
+  const T* ur = a.uref + b * a.uref_sb;
+  const Ws17<T> w(a.ws + c * full17_elems(N), N);
+  constexpr int KR_N = Ws17<T>::KR_N;
+
+  for (int e = lane; e < NZ17 * NZ17; e += 64) {
+    const int r = e / NZ17, cl = e % NZ17;
+    const T wq = (r < NX17 && cl < NX17) ? W.Q[r * NX17 + cl] : T(0);
+    const T wr = (r >= NX17 && cl >= NX17) ? W.R[(r - NX17) * NU17 + (cl - NX17)] : T(0);
+    SW[e] = s * (wq + wr);
+  }
+  __syncthreads();
+
+  T pj;
+  T Pc[NX17];   // column j of P_{k+1} (zero outside the state lanes)
+  {
+    L.v[j] = (j < NX17) ? w.XB[(int64_t)N * NX17 + jx] - xr[(int64_t)N * NX17 + jx] : T(0);
+    wave_lds_sync();
+    T acc = T(0);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) acc += W.QN[jx * NX17 + i] * L.v[i];
+    pj = (j < NX17) ? acc : T(0);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      Pc[i] = (j < NX17) ? W.QN[i * NX17 + jx] : T(0);
+      if (j < NX17) L.P[j * NX17 + i] = Pc[i];
+    }
+    wave_lds_sync();
+  }
+  bool qp_ok = true;
+  for (int k = N - 1; k >= 0; --k) {
+    T col[NX17];
+    const T* ABk = w.AB + ((int64_t)k * NZ17 + jd) * NX17;
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) col[i] = ABk[i];
+    if (j < NX17) L.gp[j] = w.GP[(int64_t)k * NX17 + j];
+    {
+      const T yb = (j < NX17) ? w.XB[(int64_t)k * NX17 + jx] : w.UB[(int64_t)k * NU17 + ju];
+      const T yr = (j < NX17) ? xr[(int64_t)k * NX17 + jx] : ur[(int64_t)k * NU17 + ju];
+      L.v[j] = dir ? yb - yr : T(0);
+    }
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) L.X[j * NX17 + i] = col[i];
+    wave_lds_sync();
+    T pt = pj;
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) pt += Pc[i] * L.gp[i];
+    L.hv[j] = (j < NX17) ? pt : T(0);
+    wave_lds_sync();
+    T hj = T(0);
+#pragma unroll
+    for (int l = 0; l < NX17; ++l) hj += col[l] * L.hv[l];
+    T y[NX17];
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) y[i] = T(0);
+    // (the asm fences keep LLVM from hoisting all 680 LDS operands of the products at once,
+    // which spilled ~500 VGPRs in fp64)
+#pragma unroll
+    for (int l = 0; l < NX17; ++l) {
+      const T cl = col[l];
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) y[i] += L.P[l * NX17 + i] * cl;
+      if (l % 4 == 3) wave_lds_sync();
+    }
+    T G[NZ17];
+#pragma unroll
+    for (int i = 0; i < NZ17; ++i) {
+      T acc = T(0);
+#pragma unroll
+      for (int l = 0; l < NX17; ++l) acc += L.X[i * NX17 + l] * y[l];
+      const T wgt = SW[jd * NZ17 + i];
+      G[i] = acc + wgt;
+      hj += wgt * L.v[i];
+      if (i % 2 == 1) wave_lds_sync();
+    }
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) L.Hu[j * NU17 + m] = G[NX17 + m];
+    wave_lds_sync();
+    L.hv[j] = hj;
+    wave_lds_sync();
+    T Huu[NU17 * NU17], hu[NU17], Lc[NU17 * NU17];
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) {
+#pragma unroll
+      for (int n = 0; n < NU17; ++n) Huu[m * NU17 + n] = L.Hu[(NX17 + n) * NU17 + m];
+      hu[m] = -L.hv[NX17 + m];
+    }
+    chol_n<T, NU17>(Huu, Lc);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) ok = ok && (Lc[i * NU17 + i] == Lc[i * NU17 + i]);
+    qp_ok = qp_ok && ok;
+    T kff[NU17], Kj[NU17], nh[NU17];
+    chol_n_solve<T, NU17>(Lc, hu, kff);
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) nh[m] = -G[NX17 + m];
+    chol_n_solve<T, NU17>(Lc, nh, Kj);
+    T pn = hj;
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) pn += G[NX17 + m] * kff[m];
+    T Pn[NX17];
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      T acc = G[i];
+#pragma unroll
+      for (int m = 0; m < NU17; ++m) acc += L.Hu[i * NU17 + m] * Kj[m];
+      Pn[i] = acc;
+    }
+    if (valid && j < NX17) {
+#pragma unroll
+      for (int m = 0; m < NU17; ++m) w.KR[(int64_t)k * KR_N + j * NU17 + m] = Kj[m];
+    }
+    if (valid && j >= NX17 && dir) w.KR[(int64_t)k * KR_N + NU17 * NX17 + ju] = sel<NU17>(kff, ju);
+    wave_lds_sync();
+    // symmetric by construction: entry (r, c) from lane max(r, c)
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) L.X[j * NX17 + i] = Pn[i];
+    pj = (j < NX17) ? pn : T(0);
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      Pc[i] = (j < NX17) ? ((i <= j) ? Pn[i] : L.X[i * NX17 + jx]) : T(0);
+      if (j < NX17) L.P[j * NX17 + i] = Pc[i];
+    }
+    wave_lds_sync();
+  }
+  __syncthreads();   // K and k are read back across lanes
+
+  // forward pass: du = K dx + k (input lanes), dx' = [A|B] (dx, du) + gap (state lanes)
+  const T* x0 = a.x0 + b * a.x0_sb;
+  T dxj = (iterate && j < NX17) ? x0[jx] - w.XB[jx] : T(0);
+  bool fin = true;
+  for (int k = 0; k < N; ++k) {
+    if (j < NX17) L.z[j] = dxj;
+    wave_lds_sync();
+    T duj = T(0);
+    if (j >= NX17 && dir) {
+      const T* Kk = w.KR + (int64_t)k * KR_N;
+      T acc = Kk[NU17 * NX17 + ju];
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) acc += Kk[i * NU17 + ju] * L.z[i];
+      duj = acc;
+      L.z[j] = duj;
+    }
+    wave_lds_sync();
+    if (valid && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + k) * NX17 + j] = w.XB[(int64_t)k * NX17 + j] + dxj;
+    if (valid && j >= NX17 && dir) {
+      const T uo = w.UB[(int64_t)k * NU17 + ju] + duj;
+      fin = fin && ((uo - uo) == T(0));
+      if (a.U) a.U[(b * (int64_t)N + k) * NU17 + ju] = uo;
+      if (k == 0) a.u0[b * NU17 + ju] = uo;
+    }
+    if (j < NX17) {
+      const T* ABk = w.AB + (int64_t)k * NZ17 * NX17;
+      T acc = w.GP[(int64_t)k * NX17 + j];
+#pragma unroll
+      for (int l = 0; l < NZ17; ++l) acc += ABk[l * NX17 + j] * L.z[l];
+      dxj = acc;
+    }
+    fin = fin && ((dxj - dxj) == T(0));
+    wave_lds_sync();
+  }
+  if (valid && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + N) * NX17 + j] = w.XB[(int64_t)N * NX17 + j] + dxj;
+  // instance status: lane 0 of the instance collects its lanes' finiteness through LDS
+  L.v[j] = fin ? T(0) : T(1);
+  wave_lds_sync();
+  if (valid && j == 0) {
+    bool all = true;
+    for (int i = 0; i < L17; ++i) all = all && (L.v[i] == T(0));
+    a.status[b] = !qp_ok ? MPCB_STATUS_QP_FAIL : (all ? MPCB_STATUS_OK : MPCB_STATUS_NAN);
+  }
+}
+
+// [A|B] of every shooting interval into dense arrays (debug / parity, mpcb_linearize).
+template <class T>
+__global__ void __launch_bounds__(64) linearize17_kernel(int64_t B, int N, T h, Model<T> M,
+                                                         const T* p, int64_t p_sb, const T* xbar,
+                                                         const T* ubar, T* A, T* Bm, T* xnext) {
+  lin17_body<T, false>(B, N, h, M, p, p_sb, xbar, ubar, 0, nullptr, 0, A, Bm, xnext);
+}
+
+template <class T>
+__global__ void __launch_bounds__(64) sim17_kernel(int64_t B, T h, Model<T> M, const T* p, int64_t p_sb,
+                                                   const T* x, const T* u, T* xo) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  P17<T> P;
+  unpack_p17(p + b * p_sb, P);
+  T xv[NX17], uv[NU17], xn[NX17];
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) xv[i] = x[b * NX17 + i];
+#pragma unroll
+  for (int m = 0; m < NU17; ++m) uv[m] = u[b * NU17 + m];
+  rk4_17<T, false>(xv, nullptr, uv, nullptr, h, M, P, xn, nullptr);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) xo[b * NX17 + i] = xn[i];
+}
+
+template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st) {
+  hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + G17 - 1) / G17)), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(riccati17_kernel<T>, dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+template <class T>
+hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
+                              const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st) {
+  const unsigned grid = (unsigned)((B * N + G17 - 1) / G17);
+  hipLaunchKernelGGL(linearize17_kernel<T>, dim3(grid), dim3(64), 0, st, B, N, h, M, p, p_sb, xbar,
+                     ubar, A, Bm, xnext);
+  return hipGetLastError();
+}
+template <class T>
+hipError_t launch_sim_step17(int64_t B, T h, const Model<T>& M, const T* p, int64_t p_sb,
+                             const T* x, const T* u, T* xo, hipStream_t st) {
+  hipLaunchKernelGGL(sim17_kernel<T>, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, h, M, p,
+                     p_sb, x, u, xo);
+  return hipGetLastError();
+}
+
+template hipError_t launch_full17<double>(const FullArgs<double>&, hipStream_t);
+template hipError_t launch_full17<float>(const FullArgs<float>&, hipStream_t);
+template hipError_t launch_linearize17<double>(int64_t, int, double, const Model<double>&, const double*,
+                                               int64_t, const double*, const double*, double*, double*,
+                                               double*, hipStream_t);
+template hipError_t launch_linearize17<float>(int64_t, int, float, const Model<float>&, const float*,
+                                              int64_t, const float*, const float*, float*, float*,
+                                              float*, hipStream_t);
+template hipError_t launch_sim_step17<double>(int64_t, double, const Model<double>&, const double*, int64_t,
+                                              const double*, const double*, double*, hipStream_t);
+template hipError_t launch_sim_step17<float>(int64_t, float, const Model<float>&, const float*, int64_t,
+                                             const float*, const float*, float*, hipStream_t);
+
+}  // namespace mpcb

@@ -1,0 +1,172 @@
+"""The full 17-state / 6-input BLASTER OCP (oracle; test infrastructure only).
+
+SURVEY §8 row f2.  The reference's actual controller (``blastermodel.py:70-292``, pinned numbers in
+``acados_ocp_blasterModel.json``: N = 60, Tf = 2, ny = 23, W = diag(Q17, R6), W_e = 10 Q17, 25
+parameters with T_blast = 21.582 at ``parameter_values[24]``):
+
+* dynamics ``f17`` (``oracle.model``, pinned to the reference's own ``generateModel()`` by
+  ``tests/golden/dynamics_ref17.npz``): the rigid body of ``f12`` plus the swivel angles
+  alpha (alpha_dot = u[4:6]) that tilt the blaster thrust T_blast through R_gimbal, and the
+  point-of-contact states (poc_dot = J_p v + J_euler eta_dot + J_angles alpha_dot);
+* RK4 with exact sensitivities of the discrete map, here by the complex step
+  (A e_j = Im Phi(x + i eps e_j) / eps, eps = 1e-30: exact to rounding, no subtraction), checked
+  against the golden analytic Jacobians of f17 at the f level;
+* the same Gauss-Newton LQ step and Riccati / active-set QP as the 12/4 slice
+  (``oracle.ocp.riccati_solve`` / ``pdas_solve`` are dimension-generic).
+
+Not covered (the device path does not implement them either): the reference's state box
+(``idxbx``, stages 1..N-1) — see DESIGN.md.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .model import Params, f17
+from .ocp import STATUS_NAN, STATUS_OK, STATUS_QP_FAIL, pdas_solve, riccati_solve
+
+NX17, NU17, NP17 = 17, 6, 25
+EPS_CS = 1e-30
+
+
+def default_Q17() -> np.ndarray:
+    # simulation_blaster.py:24 (JSON cost.W diag[0:17])
+    return np.diag([1e3] * 6 + [5.0] * 3 + [10.0] * 3 + [1e-2] * 2 + [1e3] * 3)
+
+
+def default_R6() -> np.ndarray:
+    # simulation_blaster.py:27 (JSON cost.W diag[17:23])
+    return np.diag([0.05] * 4 + [1e-5] * 2)
+
+
+def default_p25() -> np.ndarray:
+    # JSON parameter_values: all Jacobian entries 0, T_blast = 2.2 * 9.81 (simulation_blaster.py:22,67)
+    p = np.zeros(NP17)
+    p[24] = 2.2 * 9.81
+    return p
+
+
+@dataclass
+class FullSpec:
+    N: int = 60
+    dt: float = 2.0 / 60.0
+    Q: np.ndarray = field(default_factory=default_Q17)
+    R: np.ndarray = field(default_factory=default_R6)
+    QN: np.ndarray | None = None          # default 10 Q (simulation_blaster.py:25)
+    cost_scale: float | None = None       # default dt (acados time_steps)
+    lbu: np.ndarray | None = None
+    ubu: np.ndarray | None = None
+    params: Params = field(default_factory=Params)
+    max_as_iter: int = 200
+
+    def __post_init__(self):
+        if self.QN is None:
+            self.QN = 10.0 * np.asarray(self.Q)
+
+    @property
+    def s(self) -> float:
+        return self.dt if self.cost_scale is None else self.cost_scale
+
+    @property
+    def boxed(self) -> bool:
+        return self.lbu is not None
+
+
+def rk4_step17(x, u, p25, h, P: Params):
+    k1 = f17(x, u, p25, P)
+    k2 = f17(x + 0.5 * h * k1, u, p25, P)
+    k3 = f17(x + 0.5 * h * k2, u, p25, P)
+    k4 = f17(x + h * k3, u, p25, P)
+    return x + (h / 6.0) * (k1 + 2.0 * k2 + 2.0 * k3 + k4)
+
+
+def _f17c(x, u, p25, P: Params):
+    """f17 on complex arguments (the complex step); same algebra as oracle.model.f17."""
+    from .model import _rb_core, unpack_params25
+    Ja, Je, Jp, tb = unpack_params25(p25)
+    a1, a2 = x[..., 12], x[..., 13]
+    g3 = np.stack([np.sin(a1) * np.cos(a2), -np.sin(a2), np.cos(a1) * np.cos(a2)], axis=-1)
+    extra = g3 * np.asarray(tb)[..., None]
+    p_dot, eta_dot, v_dot, om_dot = _rb_core(x, u[..., 0:4], P, extra)
+    adot = u[..., 4:6]
+    poc = (np.einsum('...ij,...j->...i', Jp, x[..., 6:9]) + np.einsum('...ij,...j->...i', Je, eta_dot)
+           + np.einsum('...ij,...j->...i', Ja, adot))
+    return np.concatenate([p_dot, eta_dot, v_dot, om_dot, adot, poc], axis=-1)
+
+
+def jac17(x, u, p25, P: Params):
+    """[df/dx, df/du] of f17 by the complex step, shape (..., 17, 23)."""
+    x = np.asarray(x, dtype=np.float64)
+    u = np.asarray(u, dtype=np.float64)
+    z = np.concatenate([x, u], axis=-1)
+    out = np.empty(x.shape[:-1] + (NX17, NX17 + NU17))
+    for j in range(NX17 + NU17):
+        zc = z.astype(np.complex128)
+        zc[..., j] += 1j * EPS_CS
+        out[..., :, j] = _f17c(zc[..., :NX17], zc[..., NX17:], p25, P).imag / EPS_CS
+    return out
+
+
+def rk4_sens17(x, u, p25, h, P: Params):
+    """(x_next, A, B) of the RK4 map by the complex step (exact derivatives of the discrete map)."""
+    x = np.asarray(x, dtype=np.float64)
+    u = np.asarray(u, dtype=np.float64)
+    z = np.concatenate([x, u], axis=-1)
+    xn = rk4_step17(x, u, p25, h, P)
+    S = np.empty(x.shape[:-1] + (NX17, NX17 + NU17))
+
+    def rk4c(xc, uc):
+        k1 = _f17c(xc, uc, p25, P)
+        k2 = _f17c(xc + 0.5 * h * k1, uc, p25, P)
+        k3 = _f17c(xc + 0.5 * h * k2, uc, p25, P)
+        k4 = _f17c(xc + h * k3, uc, p25, P)
+        return xc + (h / 6.0) * (k1 + 2.0 * k2 + 2.0 * k3 + k4)
+
+    for j in range(NX17 + NU17):
+        zc = z.astype(np.complex128)
+        zc[..., j] += 1j * EPS_CS
+        S[..., :, j] = rk4c(zc[..., :NX17], zc[..., NX17:]).imag / EPS_CS
+    return xn, S[..., :, :NX17], S[..., :, NX17:]
+
+
+def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=None, ubar=None):
+    """One SQP_RTI step of the 17/6 OCP for a batch: x0 (B,17), xref (B|1,N+1,17), uref (B|1,N,6),
+    p25 (B|1,25) (acados ``set(k, 'p', p)``, the same vector on every stage)."""
+    x0 = np.asarray(x0, dtype=np.float64)
+    Bsz, N = x0.shape[0], spec.N
+    xref = np.broadcast_to(np.asarray(xref, dtype=np.float64), (Bsz, N + 1, NX17))
+    uref = np.broadcast_to(np.asarray(uref, dtype=np.float64), (Bsz, N, NU17))
+    p25 = np.broadcast_to(default_p25() if p25 is None else np.asarray(p25, dtype=np.float64),
+                          (Bsz, NP17))
+    P = spec.params
+    if mode == 'rollout':
+        ubar = uref.copy()
+        xbar = np.empty((Bsz, N + 1, NX17))
+        xbar[:, 0] = x0
+        for k in range(N):
+            xbar[:, k + 1] = rk4_step17(xbar[:, k], ubar[:, k], p25, spec.dt, P)
+    else:
+        xbar = np.asarray(xbar, dtype=np.float64)
+        ubar = np.asarray(ubar, dtype=np.float64)
+    A = np.empty((Bsz, N, NX17, NX17))
+    Bm = np.empty((Bsz, N, NX17, NU17))
+    gap = np.empty((Bsz, N, NX17))
+    for k in range(N):
+        xn, A[:, k], Bm[:, k] = rk4_sens17(xbar[:, k], ubar[:, k], p25, spec.dt, P)
+        gap[:, k] = xn - xbar[:, k + 1]
+    if mode == 'rollout':
+        gap[:] = 0.0   # the rollout is gap-free by construction
+    dx0 = x0 - xbar[:, 0]
+    if spec.boxed:
+        dx, du, status, iters = pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+    else:
+        dx, du, _, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+        status = np.where(ok, STATUS_OK, STATUS_QP_FAIL).astype(np.int32)
+        iters = np.zeros(Bsz, dtype=np.int32)
+    X = xbar + dx
+    U = ubar + du
+    bad = ~(np.isfinite(X).all(axis=(1, 2)) & np.isfinite(U).all(axis=(1, 2)))
+    status = np.where(bad, STATUS_NAN, status).astype(np.int32)
+    return dict(u0=U[:, 0].copy(), X=X, U=U, status=status, iters=iters, xbar=xbar, ubar=ubar,
+                A=A, B=Bm, gap=gap)

@@ -58,7 +58,7 @@ def rot_zyx(phi, theta, psi) -> np.ndarray:
     cf, sf = np.cos(phi), np.sin(phi)
     ct, st = np.cos(theta), np.sin(theta)
     cp, sp = np.cos(psi), np.sin(psi)
-    R = np.empty(np.shape(phi) + (3, 3))
+    R = np.empty(np.shape(phi) + (3, 3), dtype=np.result_type(phi, theta, psi, 1.0))
     R[..., 0, 0] = cp * ct
     R[..., 0, 1] = cp * st * sf - sp * cf
     R[..., 0, 2] = cp * st * cf + sp * sf
@@ -76,7 +76,7 @@ def euler_rate_inv(phi, theta) -> np.ndarray:
     cf, sf = np.cos(phi), np.sin(phi)
     ct, st = np.cos(theta), np.sin(theta)
     tt = st / ct
-    Wi = np.zeros(np.shape(phi) + (3, 3))
+    Wi = np.zeros(np.shape(phi) + (3, 3), dtype=np.result_type(phi, theta, 1.0))
     Wi[..., 0, 0] = 1.0
     Wi[..., 0, 1] = sf * tt
     Wi[..., 0, 2] = cf * tt
@@ -96,7 +96,7 @@ def _rb_core(x, T, P: Params, thrust_extra_body=None, wind=None):
     Wi = euler_rate_inv(phi, theta)
     eta_dot = np.einsum('...ij,...j->...i', Wi, om)
     Tsum = T.sum(axis=-1)
-    fb = np.zeros(np.shape(Tsum) + (3,))
+    fb = np.zeros(np.shape(Tsum) + (3,), dtype=np.result_type(Tsum, x, 1.0))
     fb[..., 2] = Tsum
     if thrust_extra_body is not None:
         fb = fb + thrust_extra_body

@@ -112,7 +112,7 @@ def _masked_stage(Huu, Hux, hu, fixed, delta):
     if fixed is not None and fixed.any():
         # free rows: h_F += H_FA delta_A
         ht = ht + np.einsum('bij,bj->bi', Huu, np.where(fixed, delta, 0.0))
-        eye = np.eye(NU)[None]
+        eye = np.eye(Huu.shape[-1])[None]
         fr = fixed[:, :, None] | fixed[:, None, :]
         diag = fixed[:, :, None] & fixed[:, None, :] & (eye > 0)
         Ht = np.where(fr, 0.0, Ht)
@@ -124,8 +124,10 @@ def _masked_stage(Huu, Hux, hu, fixed, delta):
 
 def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
                   fixed=None, delta=None):
-    """Solve the (masked) LQ QP.  Returns dx (B,N+1,NX), du (B,N,NU), mu (B,N,NU), ok (B,)."""
+    """Solve the (masked) LQ QP.  Returns dx (B,N+1,nx), du (B,N,nu), mu (B,N,nu), ok (B,).
+    Dimensions come from A (nx) and Bm (nu): the 12/4 slice and the 17/6 model share it."""
     Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
     s = spec.s
     Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
     P = np.broadcast_to(QN, (Bsz, NX, NX)).copy()
@@ -191,6 +193,7 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     Returns dx, du, status, iterations.
     """
     Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
     lb = np.broadcast_to(np.asarray(spec.lbu, dtype=np.float64), (NU,))
     ub = np.broadcast_to(np.asarray(spec.ubu, dtype=np.float64), (NU,))
     low = np.zeros((Bsz, N, NU), dtype=bool)
@@ -284,6 +287,7 @@ def dense_box_qp(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
     from scipy.optimize import lsq_linear
 
     Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
     s = spec.s
     Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
     out_du = np.empty((Bsz, N, NU))

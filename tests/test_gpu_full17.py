@@ -1,0 +1,118 @@
+"""GPU parity of the full 17/6 model path through the C ABI vs the oracle
+(oracle/full.py, whose dynamics Jacobians are pinned to the reference's generateModel()).
+
+Tolerance: fp64 per-instance ||y_dev - y_oracle||_inf / max(||y_oracle||_inf, 1) <= 1e-9 on u0,
+X and U (north_star asks 1e-5); [A|B] and the plant step <= 1e-11 absolute.  fp32 is checked on
+u0 against the fp64 oracle with a 5e-4 normwise bound (achieved 2.7e-5; the alpha-rate weight 1e-5 of the
+reference makes the 6x6 input block ill-conditioned in single precision)."""
+import numpy as np
+import pytest
+
+from oracle.full import FullSpec, default_p25, mpc_solve17, rk4_sens17, rk4_step17
+from oracle.model import Params
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, dtype=np.float64).reshape(b.shape[0], -1)
+    return np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1.0)
+
+
+def _inputs(B, N, seed):
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((B, 17))
+    x0[:, 0:3] = rng.uniform(-1, 1, (B, 3))
+    x0[:, 2] += 3.5
+    x0[:, 3:6] = rng.uniform(-0.17, 0.17, (B, 3))
+    x0[:, 6:9] = rng.uniform(-0.5, 0.5, (B, 3))
+    x0[:, 9:12] = rng.uniform(-0.087, 0.087, (B, 3))
+    x0[:, 12:14] = rng.uniform(-0.2, 0.2, (B, 2))
+    x0[:, 14:17] = rng.uniform(-0.3, 0.3, (B, 3))
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2] = 3.5
+    xref[..., 14] = 0.2            # POC_x reference (simulation_blaster.py:48)
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    p = np.tile(default_p25(), (B, 1))
+    p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
+    return x0, xref, uref, p
+
+
+def _mpc(N, dtype='f64', max_batch=64):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    return BatchedMPC(MPCConfig.full(N=N, dtype=dtype), max_batch=max_batch)
+
+
+def test_linearize17_matches_oracle():
+    N, B = 4, 5
+    m = _mpc(N, max_batch=B)
+    rng = np.random.default_rng(11)
+    x0, _, uref, p = _inputs(B, N, 11)
+    xb = x0[:, None, :] + rng.normal(0, 0.05, (B, N + 1, 17))
+    ub = uref + rng.normal(0, 0.5, (B, N, 6))
+    m.set_params(p)
+    A, Bm, xn = (t.cpu().numpy() for t in m.linearize(xb, ub))
+    P = Params()
+    for k in range(N):
+        xr, Ar, Br = rk4_sens17(xb[:, k], ub[:, k], p, 2.0 / 60.0, P)
+        assert np.abs(A[:, k] - Ar).max() < 1e-11
+        assert np.abs(Bm[:, k] - Br).max() < 1e-11
+        assert np.abs(xn[:, k] - xr).max() < 1e-11
+
+
+def test_sim_step17_matches_oracle():
+    B = 70
+    m = _mpc(10, max_batch=B)
+    x0, _, uref, p = _inputs(B, 10, 12)
+    m.set_params(p)
+    xo = m.sim_step(x0, uref[:, 0]).cpu().numpy()
+    ref = rk4_step17(x0, uref[:, 0], p, 2.0 / 60.0, Params())
+    assert np.abs(xo - ref).max() < 1e-11
+
+
+@pytest.mark.parametrize('B,N', [(1, 10), (7, 12), (33, 60)])
+def test_solve17_rollout_matches_oracle_fp64(B, N):
+    m = _mpc(N, max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 100 + B)
+    m.set_params(p)
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N), p)
+    assert (m.get_status().cpu().numpy() == o['status']).all()
+    e = [relerr(m.get_control().cpu().numpy(), o['u0']).max(),
+         relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max(),
+         relerr(m.get_input_trajectory().cpu().numpy(), o['U']).max()]
+    print(f'17/6 fp64 B={B} N={N}: u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e}')
+    assert max(e) <= 1e-9
+
+
+def test_solve17_iterate_and_default_params_match_oracle():
+    N, B = 15, 9
+    m = _mpc(N, max_batch=B)
+    x0, xref, uref, _ = _inputs(B, N, 7)
+    rng = np.random.default_rng(8)
+    xb = x0[:, None, :] + rng.normal(0, 0.05, (B, N + 1, 17))
+    ub = uref + rng.normal(0, 0.5, (B, N, 6))
+    m.set_params(None)   # defaults: zero Jacobian blocks, T_blast = 2.2 * 9.81
+    m.solve_iterate(x0, xb, ub, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N), None, mode='iterate', xbar=xb, ubar=ub)
+    assert relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max() <= 1e-9
+    assert relerr(m.get_input_trajectory().cpu().numpy(), o['U']).max() <= 1e-9
+    assert (m.get_status().cpu().numpy() == 0).all()
+
+
+def test_solve17_fp32_close_to_fp64_oracle():
+    N, B = 20, 16
+    m = _mpc(N, 'f32', max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 21)
+    m.set_params(p)
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N), p)
+    e = relerr(m.get_control().cpu().numpy(), o['u0']).max()
+    print(f'17/6 fp32 u0 err {e:.2e}')
+    assert e <= 5e-4

@@ -1,0 +1,103 @@
+"""The 17/6 oracle: dynamics Jacobians pinned to the reference's own
+generateModel() (exact sympy Jacobians in tests/golden/dynamics_ref17.npz), RK4 sensitivities
+against central differences, and the LQ step against an independent dense solve."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.full import FullSpec, default_p25, jac17, mpc_solve17, rk4_sens17, rk4_step17
+from oracle.model import Params
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def _params(d, t):
+    return Params(mass=float(d[t + '_mass']), J=d[t + '_J'], lx=float(d[t + '_lx']),
+                  ly=float(d[t + '_ly']), c=float(d[t + '_c']))
+
+
+@pytest.mark.parametrize('tag', ['sim', 'main'])
+def test_jac17_matches_reference_symbolic_jacobians(tag):
+    d = np.load(os.path.join(GOLD, 'dynamics_ref17.npz'))
+    P = _params(d, tag)
+    J = jac17(d[tag + '_x'], d[tag + '_u'], d[tag + '_p'], P)
+    for got, ref in ((J[..., :17], d[tag + '_dfdx']), (J[..., 17:], d[tag + '_dfdu'])):
+        assert np.abs(got - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
+
+
+def _random_point(B, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-0.3, 0.3, (B, 17))
+    x[:, 2] += 3.5
+    u = np.concatenate([rng.uniform(10, 30, (B, 4)), rng.uniform(-0.08, 0.08, (B, 2))], axis=1)
+    p = np.tile(default_p25(), (B, 1))
+    p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
+    return x, u, p
+
+
+def test_rk4_sens17_matches_central_differences():
+    P = Params()
+    x, u, p = _random_point(4, 1)
+    h = 1.0 / 30.0
+    _, A, Bm = rk4_sens17(x, u, p, h, P)
+    eps = 1e-6
+    for j in range(17):
+        e = np.zeros(17)
+        e[j] = eps
+        fd = (rk4_step17(x + e, u, p, h, P) - rk4_step17(x - e, u, p, h, P)) / (2 * eps)
+        assert np.abs(fd - A[:, :, j]).max() < 1e-7
+    for j in range(6):
+        e = np.zeros(6)
+        e[j] = eps
+        fd = (rk4_step17(x, u + e, p, h, P) - rk4_step17(x, u - e, p, h, P)) / (2 * eps)
+        assert np.abs(fd - Bm[:, :, j]).max() < 1e-7
+
+
+def _dense_unconstrained(o, xref, uref, spec):
+    """Condensed QP in du (dx_0 given), solved densely: an independent check of the Riccati."""
+    A, Bm, gap, xbar, ubar = o['A'], o['B'], o['gap'], o['xbar'], o['ubar']
+    Bsz, N = xbar.shape[0], spec.N
+    nx, nu = 17, 6
+    out = np.empty((Bsz, N, nu))
+    for b in range(Bsz):
+        c = np.zeros((N + 1, nx))
+        G = np.zeros((N + 1, nx, N * nu))
+        c[0] = o['X'][b, 0] - xbar[b, 0]
+        for k in range(N):
+            c[k + 1] = A[b, k] @ c[k] + gap[b, k]
+            G[k + 1] = A[b, k] @ G[k]
+            G[k + 1][:, k * nu:(k + 1) * nu] += Bm[b, k]
+        H = np.zeros((N * nu, N * nu))
+        g = np.zeros(N * nu)
+        for k in range(N + 1):
+            W = spec.QN if k == N else spec.s * spec.Q
+            e = c[k] + xbar[b, k] - xref[b, k]
+            H += G[k].T @ W @ G[k]
+            g += G[k].T @ W @ e
+        for k in range(N):
+            sl = slice(k * nu, (k + 1) * nu)
+            H[sl, sl] += spec.s * spec.R
+            g[sl] += spec.s * spec.R @ (ubar[b, k] - uref[b, k])
+        out[b] = np.linalg.solve(H, -g).reshape(N, nu)
+    return out
+
+
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_mpc_solve17_matches_dense_qp(mode):
+    N, B = 6, 3
+    spec = FullSpec(N=N)
+    x0, _, p = _random_point(B, 2)
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2] = 3.5
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    kw = {}
+    if mode == 'iterate':
+        rng = np.random.default_rng(3)
+        kw = dict(xbar=x0[:, None, :] + rng.normal(0, 0.05, (B, N + 1, 17)),
+                  ubar=uref + rng.normal(0, 0.5, (B, N, 6)))
+    o = mpc_solve17(x0, xref, uref, spec, p, mode=mode, **kw)
+    assert (o['status'] == 0).all()
+    du = _dense_unconstrained(o, xref, uref, spec)
+    assert np.abs((o['U'] - o['ubar']) - du).max() <= 1e-8 * max(1.0, np.abs(du).max())
