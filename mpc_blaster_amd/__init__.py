@@ -8,8 +8,11 @@ package is the thin host side:
 * ``compat``      — acados-subset facade (``AcadosOcpSolver`` / ``AcadosSimSolver``) and a
   ``blasterModel``-compatible constructor so reference driver loops run with an import swap.
 * ``dist``        — one process per GPU, instance sharding, RCCL gather of u0* / histograms.
+* ``load_acados_ocp_json`` — an acados OCP JSON (the reference's generated description) as an
+  ``MPCConfig`` (12/4 slice or the full 17/6 model).
 """
-from .config import MPCConfig, NX, NU  # noqa: F401
+from .acados_json import load_acados_ocp_json  # noqa: F401
+from .config import MPCConfig, NX, NU, NX17, NU17  # noqa: F401
 from ._lib import LibraryMissing, MpcbError, load as load_library  # noqa: F401
 
 
