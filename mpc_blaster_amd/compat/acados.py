@@ -11,9 +11,10 @@ Semantics kept from acados SQP_RTI (JSON ``nlp_solver_type``): one Gauss-Newton 
 is synchronous like acados'.  ``batch`` > 1 keeps B independent solvers in one object: every
 ``set``/``cost_set`` value may then carry a leading batch axis.
 
-Model slice: this build implements the 12-state/4-input rigid-body model.  Reference-length
-vectors are accepted and sliced (x[0:12]; y = [x(17); u(6)] -> x[0:12], u[0:4]); the POC /
-swivel states and the swivel-rate inputs must be zero (full model is row f2).
+Models: with a 17/6 config (``MPCConfig.full()``, ``blasterModel(..., full_model=True)``) the
+facade is the reference's own OCP — vectors pass through unchanged and ``set(k, 'p', p)``
+reaches the device parameters.  With the 12/4 rigid-body slice (the BASELINE configs) reference-
+length vectors are accepted and sliced (x[0:12]; y = [x(17); u(6)] -> x[0:12], u[0:4]).
 """
 from __future__ import annotations
 
@@ -40,20 +41,27 @@ def _as_batch(v, n, B, name):
     return np.broadcast_to(v, (B, n))
 
 
-def _slice_x(v, B, name):
+def _slice_x(v, B, name, nx=NX):
     v = np.asarray(v, dtype=np.float64)
     n = v.shape[-1] if v.ndim else 0
-    if n == NX_REF:
+    if n == NX_REF and nx == NX:
         v = v[..., :NX]
-    return _as_batch(v, NX, B, name)
+    return _as_batch(v, nx, B, name)
 
 
-def _slice_y(v, B, name):
+def _slice_u(v, B, name, nu=NU):
+    v = np.asarray(v, dtype=np.float64)
+    if v.shape[-1] == NU_REF and nu == NU:
+        v = v[..., :NU]
+    return _as_batch(v, nu, B, name)
+
+
+def _slice_y(v, B, name, nx=NX, nu=NU):
     v = np.asarray(v, dtype=np.float64)
     n = v.shape[-1]
-    if n == NX_REF + NU_REF:
+    if n == NX_REF + NU_REF and nx == NX:
         v = np.concatenate([v[..., :NX], v[..., NX_REF:NX_REF + NU]], axis=-1)
-    return _as_batch(v, NX + NU, B, name)
+    return _as_batch(v, nx + nu, B, name)
 
 
 class AcadosOcpSolver:
@@ -70,6 +78,8 @@ class AcadosOcpSolver:
         N = config.N
         dt = config.torch_dtype
         self._dev = dev
+        self.nx, self.nu = config.nx, config.nu
+        NX, NU = self.nx, self.nu
         self.xbar = torch.zeros((self.B, N + 1, NX), dtype=dt, device=dev)   # acados init: zeros
         self.ubar = torch.zeros((self.B, N, NU), dtype=dt, device=dev)
         self.x0 = np.zeros((self.B, NX))
@@ -87,7 +97,7 @@ class AcadosOcpSolver:
         if field in ('lbx', 'ubx'):
             if stage != 0:
                 raise NotImplementedError('state boxes beyond stage 0 are not part of this build')
-            v = _slice_x(value, self.B, field)
+            v = _slice_x(value, self.B, field, self.nx)
             if field == 'lbx':
                 self._lbx0 = v.copy()
             else:
@@ -95,14 +105,14 @@ class AcadosOcpSolver:
                     raise NotImplementedError('stage-0 state box must be an equality (lbx_0 == ubx_0)')
                 self.x0 = v.copy()
         elif field == 'x':
-            self.xbar[:, stage] = torch.as_tensor(_slice_x(value, self.B, 'x'), dtype=self.xbar.dtype,
-                                                  device=self._dev)
+            self.xbar[:, stage] = torch.as_tensor(_slice_x(value, self.B, 'x', self.nx),
+                                                  dtype=self.xbar.dtype, device=self._dev)
         elif field == 'u':
-            v = np.asarray(value, dtype=np.float64)
-            if v.shape[-1] == NU_REF:
-                v = v[..., :NU]
-            self.ubar[:, stage] = torch.as_tensor(_as_batch(v, NU, self.B, 'u'), dtype=self.ubar.dtype,
-                                                  device=self._dev)
+            self.ubar[:, stage] = torch.as_tensor(_slice_u(value, self.B, 'u', self.nu),
+                                                  dtype=self.ubar.dtype, device=self._dev)
+        elif field == 'p' and self.nx == NX_REF:
+            # the same vector on every stage (the reference scripts set all stages alike)
+            self.mpc.set_params(_as_batch(value, 25, self.B, 'p'))
         elif field == 'p':
             p = np.asarray(value, dtype=np.float64).reshape(-1)
             if p.size == 25 and p[24] != self.cfg.t_blast:
@@ -124,17 +134,17 @@ class AcadosOcpSolver:
         if field != 'yref':
             raise KeyError(f'cost field {field!r} not supported (weights are fixed at creation)')
         if stage == self.N:
-            self.yref[:, stage, :NX] = _slice_x(value, self.B, 'yref_e')
+            self.yref[:, stage, :self.nx] = _slice_x(value, self.B, 'yref_e', self.nx)
         else:
-            self.yref[:, stage] = _slice_y(value, self.B, 'yref')
+            self.yref[:, stage] = _slice_y(value, self.B, 'yref', self.nx, self.nu)
 
     # -------------------------------------------------------------- solve
     def solve(self) -> int:
         torch = _torch()
-        xr = self.yref[:, :, :NX]
-        ur = self.yref[:, :self.N, NX:]
+        xr = self.yref[:, :, :self.nx]
+        ur = self.yref[:, :self.N, self.nx:]
         self.mpc.solve_iterate(self.x0, self.xbar, self.ubar, xr, ur,
-                               out=(torch.empty((self.B, NU), dtype=self.xbar.dtype, device=self._dev),
+                               out=(torch.empty((self.B, self.nu), dtype=self.xbar.dtype, device=self._dev),
                                     self.xbar, self.ubar,
                                     torch.empty((self.B,), dtype=torch.int32, device=self._dev)))
         torch.cuda.synchronize(self.mpc.device)
@@ -159,9 +169,9 @@ class AcadosOcpSolver:
         R = torch.as_tensor(self.cfg.R, dtype=dt, device=self._dev)
         QN = torch.as_tensor(self.cfg.QN, dtype=dt, device=self._dev)
         yr = torch.as_tensor(self.yref, dtype=dt, device=self._dev)
-        ex = self.xbar[:, :-1] - yr[:, :-1, :NX]
-        eu = self.ubar - yr[:, :-1, NX:]
-        eN = self.xbar[:, -1] - yr[:, -1, :NX]
+        ex = self.xbar[:, :-1] - yr[:, :-1, :self.nx]
+        eu = self.ubar - yr[:, :-1, self.nx:]
+        eN = self.xbar[:, -1] - yr[:, -1, :self.nx]
         c = 0.5 * self.cfg.scale * (torch.einsum('bki,ij,bkj->b', ex, Q, ex) + torch.einsum('bki,ij,bkj->b', eu, R, eu))
         c = c + 0.5 * torch.einsum('bi,ij,bj->b', eN, QN, eN)
         c = c.cpu().numpy()
@@ -176,19 +186,19 @@ class AcadosSimSolver:
         self.cfg = config
         self.B = int(batch)
         self.mpc = BatchedMPC(config, max_batch=self.B, device=device)
-        self.x = np.zeros((self.B, NX))
-        self.u = np.zeros((self.B, NU))
+        self.nx, self.nu = config.nx, config.nu
+        self.x = np.zeros((self.B, self.nx))
+        self.u = np.zeros((self.B, self.nu))
         self.T = config.dt          # JSON Tsim = Tf/N
         self.xn = self.x.copy()
 
     def set(self, field: str, value):
         if field == 'x':
-            self.x = _slice_x(value, self.B, 'x').copy()
+            self.x = _slice_x(value, self.B, 'x', self.nx).copy()
         elif field == 'u':
-            v = np.asarray(value, dtype=np.float64)
-            if v.shape[-1] == NU_REF:
-                v = v[..., :NU]
-            self.u = _as_batch(v, NU, self.B, 'u').copy()
+            self.u = _slice_u(value, self.B, 'u', self.nu).copy()
+        elif field == 'p' and self.nx == NX_REF:
+            self.mpc.set_params(_as_batch(value, 25, self.B, 'p'))
         elif field == 'p':
             p = np.asarray(value, dtype=np.float64).reshape(-1)
             if p.size == 25 and p[24] != self.cfg.t_blast:

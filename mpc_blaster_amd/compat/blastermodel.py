@@ -3,10 +3,11 @@
 Same signature and call sequence as the reference:
 ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
 controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
-The weights / bounds given for the 17/6 reference model are sliced to the 12/4 rigid-body
-model this build implements (Q[:12,:12], R[:4,:4], thrust bounds controlBound[:, :4]).
-State bounds (statesBound) are accepted but not enforced (stage boxes are not part of the
-build; the reference scripts only pin x0).
+``full_model=True`` keeps the reference's 17/6 model and its weights unchanged (the device's
+17/6 path; input and state boxes are not applied there, with a warning).  The default keeps the
+12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4], thrust bounds
+controlBound[:, :4].  State bounds (statesBound) are accepted but not enforced (stage boxes are
+not part of the build; the reference scripts only pin x0).
 """
 from __future__ import annotations
 
@@ -14,13 +15,14 @@ import warnings
 
 import numpy as np
 
-from ..config import NU, NX, MPCConfig
+from ..config import NU, NU17, NX, NX17, MPCConfig
 from .acados import AcadosOcpSolver, AcadosSimSolver
 
 
 class blasterModel:  # noqa: N801  (reference class name)
     def __init__(self, mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
-                 controlBound, dtype: str = 'f64', batch: int = 1, device: int = 0):
+                 controlBound, dtype: str = 'f64', batch: int = 1, device: int = 0,
+                 full_model: bool = False):
         self._M = float(mass)
         self._J = np.asarray(J, dtype=np.float64)
         self._arm_length_x = float(l_x)
@@ -35,11 +37,22 @@ class blasterModel:  # noqa: N801  (reference class name)
         self._statesBound = np.asarray(statesBound, dtype=np.float64)
         self._controlBound = np.asarray(controlBound, dtype=np.float64)
         self._dtype, self._batch, self._device = dtype, int(batch), int(device)
+        self._full = bool(full_model)
         self._cfg = None
 
     def generateModel(self):
         """Builds the problem definition (the dynamics themselves live in the HIP kernels)."""
         cb = self._controlBound
+        if self._full:
+            # generateController's default parameter vector: T_blast = blastThruster * 9.81
+            # (blastermodel.py:280-282); the rest of p is set per stage by the scripts
+            self._cfg = MPCConfig(
+                N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
+                lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
+                Q=self._Q_weight[:NX17, :NX17], R=self._R_weight[:NU17, :NU17],
+                QN=self._Q_weight_t[:NX17, :NX17], t_blast=self._blastThruster * 9.81,
+                nx=NX17, nu=NU17)
+            return 0
         self._cfg = MPCConfig(
             N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
             lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
@@ -53,6 +66,9 @@ class blasterModel:  # noqa: N801  (reference class name)
     def generateController(self):
         if self._cfg is None:
             self.generateModel()
+        if self._full and self._controlBound.size:
+            warnings.warn('controlBound is not enforced on the full 17/6 model path (input boxes are '
+                          'implemented for the 12/4 slice)', stacklevel=2)
         if self._statesBound.size and np.isfinite(self._statesBound).any():
             warnings.warn('statesBound is not enforced by this build (stage state boxes are out of '
                           'scope); x0 is pinned through set(0, "lbx"/"ubx")', stacklevel=2)

@@ -116,3 +116,53 @@ def test_solve17_fp32_close_to_fp64_oracle():
     e = relerr(m.get_control().cpu().numpy(), o['u0']).max()
     print(f'17/6 fp32 u0 err {e:.2e}')
     assert e <= 5e-4
+
+
+def test_acados_facade_full_model_runs_reference_loop():
+    """simulation_blaster.py:56-107 through the compat facade on the FULL 17/6 model
+    (blasterModel(..., full_model=True)): set(0,'lbx'/'ubx'), set(k,'p'), cost_set(k,'yref'),
+    solve(), get(0,'u'), then the plant integrator — against the oracle's SQP_RTI iterate."""
+    import warnings
+    from mpc_blaster_amd.compat.blastermodel import blasterModel
+    J = np.diag([0.50781, 0.47314, 0.72975])
+    Q = np.diag([1e3] * 6 + [5.0] * 3 + [10.0] * 3 + [1e-2] * 2 + [1e3] * 3)
+    R = np.diag([5e-2] * 4 + [1e-5] * 2)
+    N = 12
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        b = blasterModel(9.0, J, 0.3434, 0.3475, N, N / 30.0, 0.03, Q, R, 10 * Q, 2.2,
+                         np.full((2, 17), np.nan), np.zeros((2, 6)), full_model=True)
+        b.generateModel()
+        integrator, ocp_solver = b.generateController()
+    rng = np.random.default_rng(4)
+    p = default_p25()
+    p[:24] = rng.uniform(-0.3, 0.3, 24)
+    x = np.zeros(17)
+    x[2] = 3.0
+    yref = np.zeros(23)
+    yref[2], yref[14] = 3.5, 0.2                      # simulation_blaster.py:48
+    spec = FullSpec(N=N)
+    xbar, ubar = np.zeros((1, N + 1, 17)), np.zeros((1, N, 6))
+    xr = np.broadcast_to(yref[:17], (1, N + 1, 17))
+    ur = np.zeros((1, N, 6))
+    for j in range(N + 1):
+        ocp_solver.set(j, 'p', p)                     # simulation_blaster.py:69
+    integrator.set('p', p)
+    for i in range(4):
+        ocp_solver.set(0, 'lbx', x)
+        ocp_solver.set(0, 'ubx', x)
+        for k in range(N + 1):
+            ocp_solver.cost_set(k, 'yref', yref if k < N else yref[:17])
+        assert ocp_solver.solve() == 0
+        u = ocp_solver.get(0, 'u')
+        o = mpc_solve17(x[None], xr, ur, spec, p[None], mode='iterate', xbar=xbar, ubar=ubar)
+        xbar, ubar = o['X'], o['U']
+        assert relerr(u[None], o['u0']).max() < 1e-9
+        assert relerr(ocp_solver.get(N, 'x')[None], o['X'][:, N]).max() < 1e-9
+        integrator.set('x', x)
+        integrator.set('u', u)
+        assert integrator.solve() == 0
+        xn = integrator.get('x')
+        ref = rk4_step17(x[None], u[None], p[None], 1.0 / 30.0, Params())[0]
+        assert np.abs(xn - ref).max() < 1e-11
+        x = xn
