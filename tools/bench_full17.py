@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Throughput of the full 17/6 model path on the reference's own OCP
+(acados_ocp_blasterModel.json: N = 60, Tf = 2, W = diag(Q17, R6), W_e = 10 Q17, T_blast =
+21.582): B instances, random x0 around hover, random per-instance POC Jacobian parameters,
+hover + POC_x = 0.2 reference (simulation_blaster.py:48).  Not a BASELINE config: the
+BASELINE metric is on the 12/4 slice (bench.py).  Prints one JSON line.
+
+    python tools/bench_full17.py [--batch 4096] [--N 60] [--dtype f64] [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=4096)
+    ap.add_argument('--N', type=int, default=60)
+    ap.add_argument('--dtype', default='f64')
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    B, N = args.batch, args.N
+    rng = np.random.default_rng(1017)
+    x0 = np.zeros((B, 17))
+    x0[:, 0:3] = rng.uniform(-1, 1, (B, 3))
+    x0[:, 2] += 3.5
+    x0[:, 3:6] = rng.uniform(-0.17, 0.17, (B, 3))
+    x0[:, 6:9] = rng.uniform(-0.5, 0.5, (B, 3))
+    x0[:, 9:12] = rng.uniform(-0.087, 0.087, (B, 3))
+    xref = np.zeros((1, N + 1, 17))
+    xref[..., 2], xref[..., 14] = 3.5, 0.2
+    uref = np.zeros((1, N, 6))
+    uref[..., :4] = 22.0725
+    p = np.zeros((B, 25))
+    p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
+    p[:, 24] = 2.2 * 9.81
+    cfg = MPCConfig.full(N=N, dtype=args.dtype)
+    m = BatchedMPC(cfg, max_batch=B)
+    dt = cfg.torch_dtype
+    dev = 'cuda:0'
+    x0t, xrt, urt, pt = (torch.as_tensor(a, dtype=dt, device=dev) for a in (x0, xref, uref, p))
+    m.set_params(pt)
+    outs = (torch.empty((B, 6), dtype=dt, device=dev), torch.empty((B, N + 1, 17), dtype=dt, device=dev),
+            torch.empty((B, N, 6), dtype=dt, device=dev), torch.empty((B,), dtype=torch.int32, device=dev))
+    for _ in range(args.warmup):
+        m.solve(x0t, xrt, urt, out=outs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.solve(x0t, xrt, urt, out=outs)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    bad = int((outs[3] != 0).sum().item())
+    print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
+                      'unit': 'solves/s', 'ms_per_step': el / args.steps * 1e3, 'batch': B,
+                      'dtype': args.dtype, 'bad_status': bad,
+                      'config': 'reference OCP (acados_ocp_blasterModel.json), random x0 + POC params'}))
+
+
+if __name__ == '__main__':
+    main()
