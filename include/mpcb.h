@@ -160,6 +160,22 @@ int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_t id_offset
  */
 int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb);
 
+/*
+ * Point-of-contact Jacobians of the blaster stream for B vehicle poses (fp64, runs on the
+ * current device / ``hip_stream``, no handle).  Replaces Jacobian_POC_Solver.solveJacobians
+ * (src/scripts/Jacobian_POC_Solver.py:222-296, htm.py:7-36): stream ODE p' = v,
+ * v' = -Mc v + g by RK4 with 10 steps, Newton ground-hit time (dT 1e-5, from 0.1, |z| <= 1e-3),
+ * forward differences with eps 1e-6.
+ *   pose   [B, 8]  phi, theta, psi, alpha1, alpha2, x, y, z (device)
+ *   Mc     host double[9], the stream drag matrix (row-major; scalar M_c -> M_c I)
+ *   poc [B,3], J_eul [B,3,3], J_mot [B,3,2], J_pos [B,3,3]; p25 [B,25] or NULL: the model
+ *   parameter vector of blastermodel.py:203-210 (vec J_mot | vec J_eul | vec J_pos | t_blast)
+ *   status [B]: 0, or MPCB_STATUS_MAXITER if a root solve hit max_iter
+ */
+int mpcb_poc_jacobians(int64_t B, const double* pose, double stream_velocity, const double* Mc,
+                       int max_iter, double t_blast, double* poc, double* J_eul, double* J_mot,
+                       double* J_pos, double* p25, int32_t* status, void* hip_stream);
+
 /* Histogram of u0 per input channel over [lo, hi) into counts[nu][nbins] (int64, accumulated). */
 int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,
                    int64_t* counts, void* hip_stream);

@@ -19,7 +19,7 @@ STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram', 'mpcb_set_timing',
-           'mpcb_last_timing', 'mpcb_set_params')
+           'mpcb_last_timing', 'mpcb_set_params', 'mpcb_poc_jacobians')
 
 
 class MpcbConfig(ctypes.Structure):
@@ -78,6 +78,8 @@ def load(path: str | None = None):
     lib.mpcb_set_timing.argtypes = [vp, i32]
     lib.mpcb_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     lib.mpcb_set_params.argtypes = [vp, vp, i64]
+    lib.mpcb_poc_jacobians.argtypes = [i64, vp, dbl, ctypes.POINTER(dbl), i32, dbl, vp, vp, vp, vp, vp,
+                                       vp, vp]
     for name in EXPORTS:
         if name not in ('mpcb_last_error', 'mpcb_workspace_bytes'):
             getattr(lib, name).restype = i32
