@@ -117,29 +117,53 @@ def run(w, world, rank, dev, steps, warmup):
     torch.cuda.synchronize()
     tdt = cfg.torch_dtype
     traj = not w['hist']
-    outs = (torch.empty((B, 4), dtype=tdt, device=dev),
-            torch.empty((B, N + 1, 12), dtype=tdt, device=dev) if traj else None,
-            torch.empty((B, N, 4), dtype=tdt, device=dev) if traj else None,
-            torch.empty((B,), dtype=torch.int32, device=dev))
-    gathered = torch.empty((world * B, 4), dtype=tdt, device=dev) if (world > 1 and traj) else None
-    counts = torch.zeros((4, 64), dtype=torch.int64, device=dev)
+
+    def make_outs():
+        return (torch.empty((B, 4), dtype=tdt, device=dev),
+                torch.empty((B, N + 1, 12), dtype=tdt, device=dev) if traj else None,
+                torch.empty((B, N, 4), dtype=tdt, device=dev) if traj else None,
+                torch.zeros((B,), dtype=torch.int32, device=dev))
+    # two output sets: with several ranks the RCCL collective of step i (async, on the process
+    # group's own stream) overlaps the solve of step i+1, which writes the other set; a set is
+    # reused only after its collective has been waited on (the compute stream waits for it)
+    nbuf = 2 if world > 1 else 1
+    out_sets = [make_outs() for _ in range(nbuf)]
+    gathered = [torch.empty((world * B, 4), dtype=tdt, device=dev) for _ in range(nbuf)] \
+        if (world > 1 and traj) else None
+    counts = [torch.zeros((4, 64), dtype=torch.int64, device=dev) for _ in range(nbuf)]
     stream = torch.cuda.current_stream()
+    pending = [None] * nbuf
+    it = [0]
 
     def step(ev=None):
+        i = it[0] % nbuf
+        it[0] += 1
+        if pending[i] is not None:
+            pending[i].wait()
+            pending[i] = None
+        o = out_sets[i]
         if ev is not None:
             ev[0].record(stream)
-        mpc.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=traj, out=outs)
+        mpc.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=traj, out=o)
         if ev is not None:
             ev[1].record(stream)
         if w['hist']:
-            counts.zero_()
-            mpc.histogram(outs[0], 0.0, 65.0, 64, counts=counts)
-            allreduce_histogram(counts)
+            counts[i].zero_()
+            mpc.histogram(o[0], 0.0, 65.0, 64, counts=counts[i])
+            if world > 1:
+                pending[i] = allreduce_histogram(counts[i], async_op=True)
         elif world > 1:
-            dist.all_gather_into_tensor(gathered, outs[0])
+            pending[i] = dist.all_gather_into_tensor(gathered[i], o[0], async_op=True)
+
+    def drain():
+        for i in range(nbuf):
+            if pending[i] is not None:
+                pending[i].wait()
+                pending[i] = None
 
     for _ in range(warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
@@ -149,12 +173,13 @@ def run(w, world, rank, dev, steps, warmup):
     t0 = time.perf_counter()
     for i in range(steps):
         step(events[i])
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    bad = int((outs[3] != 0).sum().item())
+    bad = int(sum((o[3] != 0).sum().item() for o in out_sets))
     # per-phase device time (HIP events the library records on the launch stream around each
     # kernel); a separate pass so that reading the events does not serialise the timed region
     mpc.set_timing(True)
@@ -162,6 +187,7 @@ def run(w, world, rank, dev, steps, warmup):
     for _ in range(steps):
         step()
         phases.append(mpc.last_timing())
+    drain()
     mpc.set_timing(False)
     phase_ms = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     if world > 1:

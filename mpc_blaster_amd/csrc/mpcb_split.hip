@@ -26,6 +26,10 @@
 #define MPCB_P2_DPP 1
 #endif
 
+#ifndef MPCB_P1_ALLW
+#define MPCB_P1_ALLW 1
+#endif
+
 #ifndef MPCB_P2_WAVES
 #define MPCB_P2_WAVES
 #endif
@@ -244,7 +248,12 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
   const int64_t b = a.b0 + c;
   const int N = a.N;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
+#if MPCB_P1_ALLW
+  // every lane of the quad stages the (identical) values: no exec-masked branches on the chain
+  const bool lead = true;
+#else
   const bool lead = g == 0;                        // the lane that stages the quad's values
+#endif
   const TrigQuad trig{g};
   T w[3] = {T(0), T(0), T(0)};
   if (a.wind) {

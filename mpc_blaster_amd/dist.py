@@ -60,12 +60,14 @@ def gather_u0(u0, shard: Shard, global_batch: int, group=None):
     return torch.cat(parts, dim=0)
 
 
-def allreduce_histogram(counts, group=None):
-    """Sum the per-rank int64 [nu, nbins] histograms (c5: 64 bins per motor over [0, 65])."""
+def allreduce_histogram(counts, group=None, async_op: bool = False):
+    """Sum the per-rank int64 [nu, nbins] histograms (c5: 64 bins per motor over [0, 65]).
+    ``async_op``: return the collective's work handle (None on one rank) instead of the counts."""
     import torch.distributed as dist
+    work = None
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
-    return counts
+        work = dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return work if async_op else counts
 
 
 def run_sharded(solve_fn: Callable, make_inputs_fn: Callable, global_batch: int, rank: int,
