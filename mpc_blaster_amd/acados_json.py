@@ -8,7 +8,7 @@ parts this build implements onto ``MPCConfig``:
   rigid-body slice of the BASELINE configs out of a 17/6 description);
 * LINEAR_LS cost with selector ``Vx``/``Vu`` (blastermodel.py:228-257): Q = W[:nx,:nx],
   R = W[nx:,nx:], Q_N = W_e; stage scaling = ``time_steps`` (acados' convention, uniform dt);
-* input box ``idxbu``/``lbu``/``ubu`` (blastermodel.py:259-264);
+* input box ``idxbu``/``lbu``/``ubu`` (blastermodel.py:259-264), on both models;
 * ``parameter_values`` (the default p, T_blast at p[24]);
 * ERK, 4 stages, 1 step, Gauss-Newton SQP_RTI with a full step (the only integrator / NLP
   configuration the device implements; anything else raises).
@@ -105,9 +105,6 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     phys.update(physical)
     cfg = MPCConfig(N=N, dt=dt, dtype=dtype, Q=Q, R=R, QN=We, cost_scale=dt, lbu=lbu, ubu=ubu,
                     t_blast=t_blast, nx=nx, nu=nu, **phys)
-    if nx == NX17 and lbu is not None:
-        dropped.append('input box idxbu (17/6 model: unconstrained)')
-        cfg.lbu = cfg.ubu = None
     for what in dropped:
         warnings.warn(f'acados JSON: {what} not applied by the device path', stacklevel=2)
     info = dict(yref=np.asarray(cost.get('yref', np.zeros(ny)), dtype=np.float64),

@@ -3,8 +3,8 @@
 Same signature and call sequence as the reference:
 ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
 controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
-``full_model=True`` keeps the reference's 17/6 model and its weights unchanged (the device's
-17/6 path; input and state boxes are not applied there, with a warning).  The default keeps the
+``full_model=True`` keeps the reference's 17/6 model, its weights and its input box
+(controlBound: thrusts and swivel rates) unchanged — the device's 17/6 path.  The default keeps the
 12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4], thrust bounds
 controlBound[:, :4].  State bounds (statesBound) are accepted but not enforced (stage boxes are
 not part of the build; the reference scripts only pin x0).
@@ -51,7 +51,8 @@ class blasterModel:  # noqa: N801  (reference class name)
                 lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
                 Q=self._Q_weight[:NX17, :NX17], R=self._R_weight[:NU17, :NU17],
                 QN=self._Q_weight_t[:NX17, :NX17], t_blast=self._blastThruster * 9.81,
-                nx=NX17, nu=NU17)
+                nx=NX17, nu=NU17,
+                lbu=cb[0][:NU17] if cb.size else None, ubu=cb[1][:NU17] if cb.size else None)
             return 0
         self._cfg = MPCConfig(
             N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
@@ -66,9 +67,6 @@ class blasterModel:  # noqa: N801  (reference class name)
     def generateController(self):
         if self._cfg is None:
             self.generateModel()
-        if self._full and self._controlBound.size:
-            warnings.warn('controlBound is not enforced on the full 17/6 model path (input boxes are '
-                          'implemented for the 12/4 slice)', stacklevel=2)
         if self._statesBound.size and np.isfinite(self._statesBound).any():
             warnings.warn('statesBound is not enforced by this build (stage state boxes are out of '
                           'scope); x0 is pinned through set(0, "lbx"/"ubx")', stacklevel=2)

@@ -75,7 +75,8 @@ class MPCConfig:
     def full(cls, **kw) -> 'MPCConfig':
         """The reference's own OCP (acados_ocp_blasterModel.json, simulation_blaster.py:12-30):
         17/6 model, N = 60, Tf = 2 (dt = 1/30), T_blast = 2.2 * 9.81, W = diag(Q17, R6),
-        W_e = 10 Q17.  Input/state boxes are not applied."""
+        W_e = 10 Q17.  Pass ``lbu``/``ubu`` for the reference's input box (JSON idxbu: thrusts
+        [0, 65] N, swivel rates +-0.0873 rad/s); state boxes are not applied."""
         d = dict(N=60, dt=2.0 / 60.0, t_blast=2.2 * 9.81, nx=NX17, nu=NU17)
         d.update(kw)
         return cls(**d)

@@ -139,9 +139,11 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     return fail(MPCB_E_UNSUPPORTED, "nx=%d nu=%d: implemented models are 12/4 (rigid-body slice) and 17/6 (full)",
                 cfg->nx, cfg->nu);
   if (full && cfg->box_u)
-    return fail(MPCB_E_UNSUPPORTED, "input boxes are implemented for the 12/4 model only");
+    for (int m = 0; m < NU17; ++m)
+      if (!(cfg->ubu[m] > cfg->lbu[m]))
+        return fail(MPCB_E_INVALID, "17/6 input box needs lbu < ubu (component %d)", m);
   if (cfg->N < 1 || cfg->N > 4096) return fail(MPCB_E_INVALID, "horizon N=%d out of range", cfg->N);
-  if (cfg->box_u && cfg->N > 64) return fail(MPCB_E_UNSUPPORTED, "box_u needs N <= 64 (N=%d)", cfg->N);
+  if (!full && cfg->box_u && cfg->N > 64) return fail(MPCB_E_UNSUPPORTED, "box_u needs N <= 64 (N=%d)", cfg->N);
   if (cfg->dtype != MPCB_F64 && cfg->dtype != MPCB_F32)
     return fail(MPCB_E_INVALID, "dtype=%d", cfg->dtype);
   if (!(cfg->dt > 0) || !(cfg->mass > 0)) return fail(MPCB_E_INVALID, "dt and mass must be > 0");
@@ -294,6 +296,8 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
     a.ws = (T*)h->scratch;
+    a.box = h->cfg.box_u;
+    a.max_as_iter = h->cfg.max_as_iter;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       a.b0 = b0;
       a.nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;

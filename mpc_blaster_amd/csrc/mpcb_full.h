@@ -208,11 +208,15 @@ struct FullArgs {
   const T* xbar; const T* ubar;
   T* u0; T* X; T* U; int32_t* status;
   T* ws;             // chunk workspace: per instance full17_elems(N) elements
+  int box;           // input box lbu <= u <= ubu (interior-point iterations)
+  int max_as_iter;   // iteration cap
 };
 
 __host__ __device__ constexpr int64_t full17_elems(int N) {
-  // XB (N+1)x17 | UB Nx6 | AB N x 23 columns x 17 | KR N x (6x17 + 6) | GP N x 17
-  return (int64_t)(N + 1) * NX17 + (int64_t)N * (NU17 + NZ17 * NX17 + NU17 * NX17 + NU17 + NX17);
+  // XB (N+1)x17 | UB Nx6 | AB N x 23 columns x 17 | KR N x (6x17 + 6) | GP N x 17 |
+  // input box: DX, DDX (N+1)x17 | IP N x 18 | DDU N x 6
+  return (int64_t)(N + 1) * NX17 + (int64_t)N * (NU17 + NZ17 * NX17 + NU17 * NX17 + NU17 + NX17) +
+         2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17);
 }
 
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st);

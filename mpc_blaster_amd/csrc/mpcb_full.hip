@@ -83,6 +83,7 @@ template <class T> __device__ __forceinline__ T sel17(const T* x, int i) {
 template <class T>
 struct Ws17 {
   T *XB, *UB, *AB, *KR, *GP;
+  T *DX, *DDX, *IP, *DDU;
   static constexpr int KR_N = NU17 * NX17 + NU17;
   __device__ __forceinline__ Ws17(T* ws, int N) {
     XB = ws;                                     // [N+1][17] nominal states
@@ -90,6 +91,11 @@ struct Ws17 {
     AB = UB + (int64_t)N * NU17;                 // [N][23][17] column j of [A_k|B_k] at j*17
     KR = AB + (int64_t)N * NZ17 * NX17;          // [N][6*17 + 6]: K[m][i] at i*6 + m, then k
     GP = KR + (int64_t)N * KR_N;                 // [N][17] gaps
+    // input box (interior point): iterate dx, step, (du, lambda_l, lambda_u), step du
+    DX = GP + (int64_t)N * NX17;                 // [N+1][17]
+    DDX = DX + (int64_t)(N + 1) * NX17;          // [N+1][17]
+    IP = DDX + (int64_t)(N + 1) * NX17;          // [N][18]: du | lambda_l | lambda_u
+    DDU = IP + (int64_t)N * 18;                  // [N][6]
   }
 };
 
@@ -193,43 +199,34 @@ __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
 }
 
 // ---- phases 1 + 2: Riccati backward over the cached [A|B], then the forward pass -------------
+// Shared by the unconstrained step and the interior-point iterations of the input box.  The
+// backward pass computes K_k, k_k (workspace KR) for the LQ problem around the nominal
+// trajectory shifted by (SHIFT: the current IPM iterate dx, du; else 0), with the gaps (IPM: 0)
+// and, for IPM, the barrier terms D_k (added to the diagonal of H_uu) and d_k (added to h_u).
 template <class T>
-__global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
-  __shared__ FullLds<T> lds_all[G17];
-  __shared__ T SW[NZ17 * NZ17];   // s * blkdiag(Q, R)
-  const int lane = threadIdx.x;
-  const int q = lane / L17;
-  const int j = lane % L17;
-  const bool dir = j < NZ17;                   // lane owns a direction
-  const int jd = dir ? j : 0;
-  const int jx = j < NX17 ? j : 0;
-  const int ju = (j >= NX17 && j < NZ17) ? j - NX17 : 0;
-  FullLds<T>& L = lds_all[q];
-  const int64_t c_raw = (int64_t)blockIdx.x * G17 + q;
-  const bool valid = c_raw < a.nb;
-  const int64_t c = valid ? c_raw : a.nb - 1;  // a ragged last wave shadows the last instance
-  const int64_t b = a.b0 + c;
-  const int N = a.N;
-  const T s = a.s;
-  const Weights17<T>& W = *a.W;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
-  const T* xr = a.xref + b * a.xref_sb;
-  const T* ur = a.uref + b * a.uref_sb;
-  const Ws17<T> w(a.ws + c * full17_elems(N), N);
+struct R17 {
+  FullLds<T>& L;
+  const T* SW;
+  const FullArgs<T>& a;
+  Ws17<T> w;
+  const T* xr;
+  const T* ur;
+  int j, jd, jx, ju, N;
+  bool dir, valid;
+};
+
+template <class T, bool IPM>
+__device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
+  FullLds<T>& L = r.L;
+  const int j = r.j, jd = r.jd, jx = r.jx, ju = r.ju, N = r.N;
+  const Weights17<T>& W = *r.a.W;
   constexpr int KR_N = Ws17<T>::KR_N;
-
-  for (int e = lane; e < NZ17 * NZ17; e += 64) {
-    const int r = e / NZ17, cl = e % NZ17;
-    const T wq = (r < NX17 && cl < NX17) ? W.Q[r * NX17 + cl] : T(0);
-    const T wr = (r >= NX17 && cl >= NX17) ? W.R[(r - NX17) * NU17 + (cl - NX17)] : T(0);
-    SW[e] = s * (wq + wr);
-  }
-  __syncthreads();
-
   T pj;
   T Pc[NX17];   // column j of P_{k+1} (zero outside the state lanes)
   {
-    L.v[j] = (j < NX17) ? w.XB[(int64_t)N * NX17 + jx] - xr[(int64_t)N * NX17 + jx] : T(0);
+    T xN = (j < NX17) ? r.w.XB[(int64_t)N * NX17 + jx] : T(0);
+    if (IPM && j < NX17) xN += r.w.DX[(int64_t)N * NX17 + jx];
+    L.v[j] = (j < NX17) ? xN - r.xr[(int64_t)N * NX17 + jx] : T(0);
     wave_lds_sync();
     T acc = T(0);
 #pragma unroll
@@ -245,14 +242,15 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
   bool qp_ok = true;
   for (int k = N - 1; k >= 0; --k) {
     T col[NX17];
-    const T* ABk = w.AB + ((int64_t)k * NZ17 + jd) * NX17;
+    const T* ABk = r.w.AB + ((int64_t)k * NZ17 + jd) * NX17;
 #pragma unroll
     for (int i = 0; i < NX17; ++i) col[i] = ABk[i];
-    if (j < NX17) L.gp[j] = w.GP[(int64_t)k * NX17 + j];
+    if (j < NX17) L.gp[j] = IPM ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
     {
-      const T yb = (j < NX17) ? w.XB[(int64_t)k * NX17 + jx] : w.UB[(int64_t)k * NU17 + ju];
-      const T yr = (j < NX17) ? xr[(int64_t)k * NX17 + jx] : ur[(int64_t)k * NU17 + ju];
-      L.v[j] = dir ? yb - yr : T(0);
+      T yb = (j < NX17) ? r.w.XB[(int64_t)k * NX17 + jx] : r.w.UB[(int64_t)k * NU17 + ju];
+      if constexpr (IPM) yb += (j < NX17) ? r.w.DX[(int64_t)k * NX17 + jx] : r.w.IP[(int64_t)k * 18 + ju];
+      const T yr = (j < NX17) ? r.xr[(int64_t)k * NX17 + jx] : r.ur[(int64_t)k * NU17 + ju];
+      L.v[j] = r.dir ? yb - yr : T(0);
     }
 #pragma unroll
     for (int i = 0; i < NX17; ++i) L.X[j * NX17 + i] = col[i];
@@ -268,8 +266,6 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     T y[NX17];
 #pragma unroll
     for (int i = 0; i < NX17; ++i) y[i] = T(0);
-    // (the asm fences keep LLVM from hoisting all 680 LDS operands of the products at once,
-    // which spilled ~500 VGPRs in fp64)
 #pragma unroll
     for (int l = 0; l < NX17; ++l) {
       const T cl = col[l];
@@ -283,7 +279,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       T acc = T(0);
 #pragma unroll
       for (int l = 0; l < NX17; ++l) acc += L.X[i * NX17 + l] * y[l];
-      const T wgt = SW[jd * NZ17 + i];
+      const T wgt = r.SW[jd * NZ17 + i];
       G[i] = acc + wgt;
       hj += wgt * L.v[i];
       if (i % 2 == 1) wave_lds_sync();
@@ -293,12 +289,22 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     wave_lds_sync();
     L.hv[j] = hj;
     wave_lds_sync();
-    T Huu[NU17 * NU17], hu[NU17], Lc[NU17 * NU17];
+    T Huu[NU17 * NU17], ht[NU17], Lc[NU17 * NU17];
 #pragma unroll
     for (int m = 0; m < NU17; ++m) {
 #pragma unroll
       for (int n = 0; n < NU17; ++n) Huu[m * NU17 + n] = L.Hu[(NX17 + n) * NU17 + m];
-      hu[m] = -L.hv[NX17 + m];
+      ht[m] = L.hv[NX17 + m];
+    }
+    if constexpr (IPM) {   // barrier terms of this stage (instance-uniform values)
+      const T* ip = r.w.IP + (int64_t)k * 18;
+#pragma unroll
+      for (int m = 0; m < NU17; ++m) {
+        const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+        const T sl = ip[m] - (W.lbu[m] - ubk), su = (W.ubu[m] - ubk) - ip[m];
+        Huu[m * NU17 + m] += ip[6 + m] / sl + ip[12 + m] / su;
+        ht[m] -= smu * (T(1) / sl - T(1) / su);
+      }
     }
     chol_n<T, NU17>(Huu, Lc);
     bool ok = true;
@@ -306,7 +312,9 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     for (int i = 0; i < NU17; ++i) ok = ok && (Lc[i * NU17 + i] == Lc[i * NU17 + i]);
     qp_ok = qp_ok && ok;
     T kff[NU17], Kj[NU17], nh[NU17];
-    chol_n_solve<T, NU17>(Lc, hu, kff);
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) nh[m] = -ht[m];
+    chol_n_solve<T, NU17>(Lc, nh, kff);
 #pragma unroll
     for (int m = 0; m < NU17; ++m) nh[m] = -G[NX17 + m];
     chol_n_solve<T, NU17>(Lc, nh, Kj);
@@ -321,11 +329,11 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       for (int m = 0; m < NU17; ++m) acc += L.Hu[i * NU17 + m] * Kj[m];
       Pn[i] = acc;
     }
-    if (valid && j < NX17) {
+    if (r.valid && j < NX17) {
 #pragma unroll
-      for (int m = 0; m < NU17; ++m) w.KR[(int64_t)k * KR_N + j * NU17 + m] = Kj[m];
+      for (int m = 0; m < NU17; ++m) r.w.KR[(int64_t)k * KR_N + j * NU17 + m] = Kj[m];
     }
-    if (valid && j >= NX17 && dir) w.KR[(int64_t)k * KR_N + NU17 * NX17 + ju] = sel<NU17>(kff, ju);
+    if (r.valid && j >= NX17 && r.dir) r.w.KR[(int64_t)k * KR_N + NU17 * NX17 + ju] = sel<NU17>(kff, ju);
     wave_lds_sync();
     // symmetric by construction: entry (r, c) from lane max(r, c)
 #pragma unroll
@@ -339,35 +347,51 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     }
     wave_lds_sync();
   }
-  __syncthreads();   // K and k are read back across lanes
+  return qp_ok;
+}
 
-  // forward pass: du = K dx + k (input lanes), dx' = [A|B] (dx, du) + gap (state lanes)
-  const T* x0 = a.x0 + b * a.x0_sb;
-  T dxj = (iterate && j < NX17) ? x0[jx] - w.XB[jx] : T(0);
+// Forward pass over K, k.  GAIN: du = K dx + k; else du from the IPM iterate (the initial
+// trajectory).  STEP: the Newton step (zero gaps, dx_0 = 0) into the workspace DDX / DDU.
+// Returns this lane's finiteness; writes X / U / u0 when OUT.
+template <class T, bool GAIN, bool STEP, bool OUT>
+__device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
+  FullLds<T>& L = r.L;
+  const int j = r.j, ju = r.ju, N = r.N;
+  const FullArgs<T>& a = r.a;
+  constexpr int KR_N = Ws17<T>::KR_N;
+  const bool ilane = j >= NX17 && r.dir;
+  const int64_t b = a.b0 + (r.w.XB - a.ws) / full17_elems(N);
   bool fin = true;
   for (int k = 0; k < N; ++k) {
     if (j < NX17) L.z[j] = dxj;
     wave_lds_sync();
     T duj = T(0);
-    if (j >= NX17 && dir) {
-      const T* Kk = w.KR + (int64_t)k * KR_N;
-      T acc = Kk[NU17 * NX17 + ju];
+    if (ilane) {
+      if constexpr (GAIN) {
+        const T* Kk = r.w.KR + (int64_t)k * KR_N;
+        T acc = Kk[NU17 * NX17 + ju];
 #pragma unroll
-      for (int i = 0; i < NX17; ++i) acc += Kk[i * NU17 + ju] * L.z[i];
-      duj = acc;
+        for (int i = 0; i < NX17; ++i) acc += Kk[i * NU17 + ju] * L.z[i];
+        duj = acc;
+      } else {
+        duj = r.w.IP[(int64_t)k * 18 + ju];
+      }
       L.z[j] = duj;
     }
     wave_lds_sync();
-    if (valid && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + k) * NX17 + j] = w.XB[(int64_t)k * NX17 + j] + dxj;
-    if (valid && j >= NX17 && dir) {
-      const T uo = w.UB[(int64_t)k * NU17 + ju] + duj;
+    if (STEP && r.valid && j < NX17) r.w.DDX[(int64_t)k * NX17 + j] = dxj;
+    if (STEP && r.valid && ilane) r.w.DDU[(int64_t)k * NU17 + ju] = duj;
+    if (!STEP && !OUT && r.valid && j < NX17) r.w.DX[(int64_t)k * NX17 + j] = dxj;
+    if (OUT && write && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + k) * NX17 + j] = r.w.XB[(int64_t)k * NX17 + j] + dxj;
+    if (ilane) {
+      const T uo = r.w.UB[(int64_t)k * NU17 + ju] + duj;
       fin = fin && ((uo - uo) == T(0));
-      if (a.U) a.U[(b * (int64_t)N + k) * NU17 + ju] = uo;
-      if (k == 0) a.u0[b * NU17 + ju] = uo;
+      if (OUT && write && a.U) a.U[(b * (int64_t)N + k) * NU17 + ju] = uo;
+      if (OUT && write && k == 0) a.u0[b * NU17 + ju] = uo;
     }
     if (j < NX17) {
-      const T* ABk = w.AB + (int64_t)k * NZ17 * NX17;
-      T acc = w.GP[(int64_t)k * NX17 + j];
+      const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
+      T acc = STEP ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
 #pragma unroll
       for (int l = 0; l < NZ17; ++l) acc += ABk[l * NX17 + j] * L.z[l];
       dxj = acc;
@@ -375,14 +399,157 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     fin = fin && ((dxj - dxj) == T(0));
     wave_lds_sync();
   }
-  if (valid && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + N) * NX17 + j] = w.XB[(int64_t)N * NX17 + j] + dxj;
+  if (STEP && r.valid && j < NX17) r.w.DDX[(int64_t)N * NX17 + j] = dxj;
+  if (!STEP && !OUT && r.valid && j < NX17) r.w.DX[(int64_t)N * NX17 + j] = dxj;
+  if (OUT && write && j < NX17 && a.X) a.X[(b * (int64_t)(N + 1) + N) * NX17 + j] = r.w.XB[(int64_t)N * NX17 + j] + dxj;
+  return fin;
+}
+
+constexpr double IPM17_SIGMA = 0.1, IPM17_TAU = 0.995, IPM17_THETA = 0.1, IPM17_TOL = 1e-12;
+
+// BOX: the input box lbu <= u <= ubu of the reference OCP (blastermodel.py:259-264; thrust
+// [0, 65] N, swivel rate +-0.0873 rad/s) by a primal-dual interior point over the Riccati
+// recursion (acados uses HPIPM's; oracle.ocp.ipm_box_solve is the same iteration): Newton steps
+// of the barrier-perturbed KKT system linearised at the current iterate (input Hessian + D,
+// gradient - sigma mu (1/s_l - 1/s_u)), a common primal/dual step length tau to the boundary,
+// until mu = mean(lambda s) <= 1e-12.  (The exact active set of the 12/4 path needs thousands of
+// exchanges on this model: the swivel-rate weight is 1e-5.)
+template <class T, bool BOX>
+__global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
+  __shared__ FullLds<T> lds_all[G17];
+  __shared__ T SW[NZ17 * NZ17];   // s * blkdiag(Q, R)
+  const int lane = threadIdx.x;
+  const int q = lane / L17;
+  const int j = lane % L17;
+  const int64_t c_raw = (int64_t)blockIdx.x * G17 + q;
+  const bool valid = c_raw < a.nb;
+  const int64_t c = valid ? c_raw : a.nb - 1;  // a ragged last wave shadows the last instance
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const Weights17<T>& W = *a.W;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const bool dir = j < NZ17;
+  const R17<T> r{lds_all[q], SW, a, Ws17<T>(a.ws + c * full17_elems(N), N), a.xref + b * a.xref_sb,
+                 a.uref + b * a.uref_sb, j, dir ? j : 0, j < NX17 ? j : 0,
+                 (j >= NX17 && dir) ? j - NX17 : 0, N, dir, valid};
+  FullLds<T>& L = r.L;
+  const bool ilane = j >= NX17 && dir;
+  const int ju = r.ju;
+  for (int e = lane; e < NZ17 * NZ17; e += 64) {
+    const int rr = e / NZ17, cl = e % NZ17;
+    const T wq = (rr < NX17 && cl < NX17) ? W.Q[rr * NX17 + cl] : T(0);
+    const T wr = (rr >= NX17 && cl >= NX17) ? W.R[(rr - NX17) * NU17 + (cl - NX17)] : T(0);
+    SW[e] = a.s * (wq + wr);
+  }
+  __syncthreads();
+  const T* x0 = a.x0 + b * a.x0_sb;
+  const T dx0 = (iterate && j < NX17) ? x0[r.jx] - r.w.XB[r.jx] : T(0);
+  int32_t st = MPCB_STATUS_OK;
+  bool fin;
+  if constexpr (!BOX) {
+    if (!riccati17_backward<T, false>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
+    __syncthreads();   // K and k are read back across lanes
+    fin = forward17<T, true, false, true>(r, dx0, valid);
+  } else {
+    const T lbm = W.lbu[ju], ubm = W.ubu[ju];
+    // start: du strictly inside the box, lambda = 1; dx by the dynamics
+    if (valid && ilane) {
+      for (int k = 0; k < N; ++k) {
+        const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
+        const T lb = lbm - ubk, ub = ubm - ubk, wd = ub - lb;
+        T* ip = r.w.IP + (int64_t)k * 18;
+        ip[ju] = fmin(fmax(T(0), lb + T(IPM17_THETA) * wd), ub - T(IPM17_THETA) * wd);
+        ip[6 + ju] = T(1);
+        ip[12 + ju] = T(1);
+      }
+    }
+    __syncthreads();
+    forward17<T, false, false, false>(r, dx0, false);   // DX of the starting point
+    __syncthreads();
+    bool done = false;
+    for (int it = 0; it < a.max_as_iter; ++it) {
+      // duality measure mu = mean(lambda s) (input lanes sum over stages, then over components)
+      T part = T(0);
+      if (ilane) {
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
+          const T* ip = r.w.IP + (int64_t)k * 18;
+          part += ip[6 + ju] * (ip[ju] - (lbm - ubk)) + ip[12 + ju] * ((ubm - ubk) - ip[ju]);
+        }
+      }
+      T mu = T(0);
+#pragma unroll
+      for (int m = 0; m < NU17; ++m) mu += __shfl(part, q * L17 + NX17 + m);
+      mu /= T(2 * N * NU17);
+      done = done || !(mu > T(IPM17_TOL));
+      if (__all(done || !valid)) break;
+      const T smu = T(IPM17_SIGMA) * mu;
+      if (!riccati17_backward<T, true>(r, smu)) st = MPCB_STATUS_QP_FAIL;
+      __syncthreads();
+      forward17<T, true, true, false>(r, T(0), false);   // the Newton step -> DDX, DDU
+      __syncthreads();
+      // step length: fraction tau to the boundary, primal and dual, common to the instance
+      T amax = T(1) / T(IPM17_TAU);
+      if (ilane) {
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
+          const T* ip = r.w.IP + (int64_t)k * 18;
+          const T d = r.w.DDU[(int64_t)k * NU17 + ju];
+          const T sl = ip[ju] - (lbm - ubk), su = (ubm - ubk) - ip[ju];
+          const T ll = ip[6 + ju], lu = ip[12 + ju];
+          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          if (d < T(0)) amax = fmin(amax, -sl / d);
+          if (d > T(0)) amax = fmin(amax, su / d);
+          if (dll < T(0)) amax = fmin(amax, -ll / dll);
+          if (dlu < T(0)) amax = fmin(amax, -lu / dlu);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NU17; ++m) amax = fmin(amax, __shfl(amax, q * L17 + NX17 + m));
+      const T alpha = done ? T(0) : fmin(T(1), T(IPM17_TAU) * amax);
+      if (valid && ilane) {
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
+          T* ip = r.w.IP + (int64_t)k * 18;
+          const T d = r.w.DDU[(int64_t)k * NU17 + ju];
+          const T sl = ip[ju] - (lbm - ubk), su = (ubm - ubk) - ip[ju];
+          const T ll = ip[6 + ju], lu = ip[12 + ju];
+          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          ip[ju] += alpha * d;
+          ip[6 + ju] = ll + alpha * dll;
+          ip[12 + ju] = lu + alpha * dlu;
+        }
+      }
+      if (valid && j < NX17) {
+        for (int k = 0; k <= N; ++k) r.w.DX[(int64_t)k * NX17 + j] += alpha * r.w.DDX[(int64_t)k * NX17 + j];
+      }
+      __syncthreads();
+    }
+    if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+    // outputs: X = xbar + dx, U = ubar + du of the final iterate
+    fin = true;
+    for (int k = 0; k <= N; ++k) {
+      if (valid && j < NX17 && a.X)
+        a.X[(b * (int64_t)(N + 1) + k) * NX17 + j] = r.w.XB[(int64_t)k * NX17 + j] + r.w.DX[(int64_t)k * NX17 + j];
+      if (ilane && k < N) {
+        const T uo = r.w.UB[(int64_t)k * NU17 + ju] + r.w.IP[(int64_t)k * 18 + ju];
+        fin = fin && ((uo - uo) == T(0));
+        if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + ju] = uo;
+        if (valid && k == 0) a.u0[b * NU17 + ju] = uo;
+      }
+      if (j < NX17) {
+        const T xo = r.w.DX[(int64_t)k * NX17 + j];
+        fin = fin && ((xo - xo) == T(0));
+      }
+    }
+  }
   // instance status: lane 0 of the instance collects its lanes' finiteness through LDS
   L.v[j] = fin ? T(0) : T(1);
   wave_lds_sync();
   if (valid && j == 0) {
     bool all = true;
     for (int i = 0; i < L17; ++i) all = all && (L.v[i] == T(0));
-    a.status[b] = !qp_ok ? MPCB_STATUS_QP_FAIL : (all ? MPCB_STATUS_OK : MPCB_STATUS_NAN);
+    a.status[b] = !all ? MPCB_STATUS_NAN : st;
   }
 }
 
@@ -414,7 +581,10 @@ __global__ void __launch_bounds__(64) sim17_kernel(int64_t B, T h, Model<T> M, c
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st) {
   hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
   hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + G17 - 1) / G17)), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(riccati17_kernel<T>, dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
+  if (a.box)
+    hipLaunchKernelGGL((riccati17_kernel<T, true>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL((riccati17_kernel<T, false>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 template <class T>

@@ -11,10 +11,12 @@ parameters with T_blast = 21.582 at ``parameter_values[24]``):
 * RK4 with exact sensitivities of the discrete map, here by the complex step
   (A e_j = Im Phi(x + i eps e_j) / eps, eps = 1e-30: exact to rounding, no subtraction), checked
   against the golden analytic Jacobians of f17 at the f level;
-* the same Gauss-Newton LQ step and Riccati / active-set QP as the 12/4 slice
-  (``oracle.ocp.riccati_solve`` / ``pdas_solve`` are dimension-generic).
+* the same Gauss-Newton LQ step and Riccati recursion as the 12/4 slice
+  (``oracle.ocp.riccati_solve`` is dimension-generic); the input box (JSON idxbu) by the
+  primal-dual interior point ``oracle.ocp.ipm_box_solve`` (acados uses HPIPM's interior point;
+  the exact active set of the 12/4 path needs thousands of exchanges on this model).
 
-Not covered (the device path does not implement them either): the reference's state box
+Not covered (the device path does not implement it either): the reference's state box
 (``idxbx``, stages 1..N-1) — see DESIGN.md.
 """
 from __future__ import annotations
@@ -24,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .model import Params, f17
-from .ocp import STATUS_NAN, STATUS_OK, STATUS_QP_FAIL, pdas_solve, riccati_solve
+from .ocp import STATUS_NAN, STATUS_OK, STATUS_QP_FAIL, ipm_box_solve, riccati_solve
 
 NX17, NU17, NP17 = 17, 6, 25
 EPS_CS = 1e-30
@@ -158,8 +160,9 @@ def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=N
     if mode == 'rollout':
         gap[:] = 0.0   # the rollout is gap-free by construction
     dx0 = x0 - xbar[:, 0]
-    if spec.boxed:
-        dx, du, status, iters = pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+    if spec.boxed:   # interior point (the active set needs thousands of exchanges here)
+        dx, du, status, iters = ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec,
+                                              max_iter=spec.max_as_iter)
     else:
         dx, du, _, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
         status = np.where(ok, STATUS_OK, STATUS_QP_FAIL).astype(np.int32)

@@ -123,9 +123,11 @@ def _masked_stage(Huu, Hux, hu, fixed, delta):
 
 
 def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
-                  fixed=None, delta=None):
+                  fixed=None, delta=None, Rd=None, rd=None):
     """Solve the (masked) LQ QP.  Returns dx (B,N+1,nx), du (B,N,nu), mu (B,N,nu), ok (B,).
-    Dimensions come from A (nx) and Bm (nu): the 12/4 slice and the 17/6 model share it."""
+    Dimensions come from A (nx) and Bm (nu): the 12/4 slice and the 17/6 model share it.
+    Rd, rd (B,N,nu): extra diagonal input Hessian and input gradient per stage (the barrier
+    terms of ``ipm_box_solve``)."""
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
     s = spec.s
@@ -148,6 +150,9 @@ def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
         Huu = s * R + np.einsum('bji,bjk->bik', Bk, PB)
         hx = s * np.einsum('ij,bj->bi', Q, xbar[:, k] - xref[:, k]) + np.einsum('bji,bj->bi', Ak, pt)
         hu = s * np.einsum('ij,bj->bi', R, ubar[:, k] - uref[:, k]) + np.einsum('bji,bj->bi', Bk, pt)
+        if Rd is not None:
+            Huu = Huu + Rd[:, k, :, None] * np.eye(NU)[None]
+            hu = hu + rd[:, k]
         fk = None if fixed is None else fixed[:, k]
         dk = None if delta is None else delta[:, k]
         Ht, Hxt, ht = _masked_stage(Huu, Hux, hu, fk, dk)
@@ -238,6 +243,70 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     status = np.where(done, STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
     return out_dx, out_du, status, iters
+
+
+IPM_SIGMA, IPM_TAU, IPM_THETA, IPM_TOL = 0.1, 0.995, 0.1, 1e-12
+
+
+def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60):
+    """Input-box QP by a primal-dual interior point over the Riccati recursion (the method of
+    acados' HPIPM; used for the full 17/6 model, where the active set above can need thousands
+    of exchanges).  Iterate (du, dx, lambda_l, lambda_u) with du strictly inside
+    [lb, ub] = [lbu - ubar, ubu - ubar] and dx consistent with the dynamics.  Every iteration
+    takes the Newton step of the barrier-perturbed KKT system: the LQ problem in the step
+    (Delta x, Delta u) LINEARISED AT THE CURRENT ITERATE (references shifted by (dx, du), zero
+    gaps, Delta x_0 = 0 — so the step never comes out of a difference of large numbers when
+    D = lambda_l/s_l + lambda_u/s_u grows at active bounds) with input Hessian + D and input
+    gradient - sigma mu (1/s_l - 1/s_u); then a fraction tau of the way to the boundary in the
+    primal and dual variables (common length).  Start: du = clip(0, lb + theta w, ub - theta w)
+    (dx by the dynamics), lambda = 1.  Stops when mu = mean(lambda s) <= IPM_TOL or after
+    ``max_iter`` iterations.  Returns dx, du, status, iterations."""
+    Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
+    lb = np.asarray(spec.lbu, dtype=np.float64) - ubar
+    ub = np.asarray(spec.ubu, dtype=np.float64) - ubar
+    w = ub - lb
+    du = np.clip(np.zeros_like(lb), lb + IPM_THETA * w, ub - IPM_THETA * w)
+    dx = np.empty((Bsz, N + 1, NX))
+    dx[:, 0] = dx0
+    for k in range(N):
+        dx[:, k + 1] = np.einsum('bij,bj->bi', A[:, k], dx[:, k]) + np.einsum('bij,bj->bi', Bm[:, k], du[:, k]) + gap[:, k]
+    ll = np.ones_like(du)
+    lu = np.ones_like(du)
+    it = np.zeros(Bsz, dtype=np.int32)
+    ok = np.ones(Bsz, dtype=bool)
+    act = np.ones(Bsz, dtype=bool)
+    zgap = np.zeros_like(gap)
+    zdx0 = np.zeros_like(dx0)
+    for _ in range(max_iter):
+        sl, su = du - lb, ub - du
+        mu = (ll * sl + lu * su).sum(axis=(1, 2)) / (2 * N * NU)
+        act = act & (mu > IPM_TOL)
+        if not act.any():
+            break
+        smu = (IPM_SIGMA * mu)[:, None, None]
+        D = ll / sl + lu / su
+        d = -smu * (1.0 / sl - 1.0 / su)
+        ddx, dd, _, ok2 = riccati_solve(A, Bm, zgap, zdx0, xbar + dx, ubar + du, xref, uref, spec, Rd=D, rd=d)
+        ok &= ok2 | ~act
+        dll = (smu - ll * sl - ll * dd) / sl
+        dlu = (smu - lu * su + lu * dd) / su
+        with np.errstate(divide='ignore', invalid='ignore'):
+            ap = np.where(dd < 0, -sl / dd, np.where(dd > 0, su / dd, np.inf)).min(axis=(1, 2))
+            ad = np.minimum(np.where(dll < 0, -ll / dll, np.inf).min(axis=(1, 2)),
+                            np.where(dlu < 0, -lu / dlu, np.inf).min(axis=(1, 2)))
+        alpha = np.minimum(1.0, IPM_TAU * np.minimum(ap, ad))
+        alpha = np.where(act, alpha, 0.0)[:, None, None]
+        du = du + alpha * dd
+        dx = dx + alpha * ddx
+        ll = ll + alpha * dll
+        lu = lu + alpha * dlu
+        it += act
+    sl, su = du - lb, ub - du
+    mu = (ll * sl + lu * su).sum(axis=(1, 2)) / (2 * N * NU)
+    status = np.where(mu <= IPM_TOL, STATUS_OK, STATUS_MAXITER).astype(np.int32)
+    status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
+    return dx, du, status, it
 
 
 def mpc_solve(x0, xref, uref, spec: OcpSpec, wind=None, mode='rollout', xbar=None, ubar=None,

@@ -33,7 +33,8 @@ def test_full_model_matches_reference_defaults():
     assert cfg.t_blast == pytest.approx(21.582, rel=1e-12)
     assert info['idxbx'] == list(range(17)) and len(info['lbx']) == 17
     assert any('state box' in str(x.message) for x in w)
-    assert cfg.lbu is None   # 17/6: input boxes not applied (reported)
+    assert np.array_equal(cfg.lbu, [0, 0, 0, 0, -0.0872665, -0.0872665])
+    assert np.array_equal(cfg.ubu, [65, 65, 65, 65, 0.0872665, 0.0872665])
 
 
 def test_slice_12_4_matches_baseline_config():

@@ -14,6 +14,9 @@ from oracle.model import Params
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
+LBU17 = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])   # JSON idxbu/lbu/ubu
+UBU17 = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+
 
 def relerr(a, b):
     a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
@@ -120,8 +123,9 @@ def test_solve17_fp32_close_to_fp64_oracle():
 
 def test_acados_facade_full_model_runs_reference_loop():
     """simulation_blaster.py:56-107 through the compat facade on the FULL 17/6 model
-    (blasterModel(..., full_model=True)): set(0,'lbx'/'ubx'), set(k,'p'), cost_set(k,'yref'),
-    solve(), get(0,'u'), then the plant integrator — against the oracle's SQP_RTI iterate."""
+    (blasterModel(..., full_model=True), the reference's controlBound enforced): set(0,'lbx'/'ubx'),
+    set(k,'p'), cost_set(k,'yref'), solve(), get(0,'u'), then the plant integrator — against the
+    oracle's SQP_RTI iterate."""
     import warnings
     from mpc_blaster_amd.compat.blastermodel import blasterModel
     J = np.diag([0.50781, 0.47314, 0.72975])
@@ -131,7 +135,7 @@ def test_acados_facade_full_model_runs_reference_loop():
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
         b = blasterModel(9.0, J, 0.3434, 0.3475, N, N / 30.0, 0.03, Q, R, 10 * Q, 2.2,
-                         np.full((2, 17), np.nan), np.zeros((2, 6)), full_model=True)
+                         np.full((2, 17), np.nan), np.stack([LBU17, UBU17]), full_model=True)
         b.generateModel()
         integrator, ocp_solver = b.generateController()
     rng = np.random.default_rng(4)
@@ -141,7 +145,7 @@ def test_acados_facade_full_model_runs_reference_loop():
     x[2] = 3.0
     yref = np.zeros(23)
     yref[2], yref[14] = 3.5, 0.2                      # simulation_blaster.py:48
-    spec = FullSpec(N=N)
+    spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17)          # controlBound (simulation_blaster.py:30)
     xbar, ubar = np.zeros((1, N + 1, 17)), np.zeros((1, N, 6))
     xr = np.broadcast_to(yref[:17], (1, N + 1, 17))
     ur = np.zeros((1, N, 6))
@@ -166,3 +170,43 @@ def test_acados_facade_full_model_runs_reference_loop():
         ref = rk4_step17(x[None], u[None], p[None], 1.0 / 30.0, Params())[0]
         assert np.abs(xn - ref).max() < 1e-11
         x = xn
+
+
+
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_solve17_input_box_matches_oracle_interior_point(mode):
+    """The reference's input box on the full model by the interior point: the device iterate
+    equals the oracle's (same iteration, <= 1e-9; achieved ~1e-13) and both match an independent dense box-QP solve (SciPy BVLS on the condensed
+    problem, <= 1e-5: its own accuracy on this ill-conditioned Hessian)."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    from oracle.ocp import dense_box_qp
+    N, B = 20, 24
+    m = BatchedMPC(MPCConfig.full(N=N, lbu=LBU17, ubu=UBU17), max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 31)
+    m.set_params(p)
+    spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17)
+    kw = {}
+    if mode == 'iterate':
+        rng = np.random.default_rng(32)
+        kw = dict(xbar=x0[:, None, :] + rng.normal(0, 0.05, (B, N + 1, 17)),
+                  ubar=uref + rng.normal(0, 0.5, (B, N, 6)))
+        m.solve_iterate(x0, kw['xbar'], kw['ubar'], xref, uref)
+    else:
+        m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, spec, p, mode=mode, **kw)
+    assert (o['status'] == 0).all()
+    assert (m.get_status().cpu().numpy() == 0).all()
+    U = m.get_input_trajectory().cpu().numpy()
+    assert (U >= LBU17 - 1e-9).all() and (U <= UBU17 + 1e-9).all()
+    act = np.isclose(o['U'], LBU17, atol=1e-6) | np.isclose(o['U'], UBU17, atol=1e-6)
+    assert act.any()                                   # the box is active somewhere
+    e = [relerr(m.get_control().cpu().numpy(), o['u0']).max(),
+         relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max(), relerr(U, o['U']).max()]
+    dd = dense_box_qp(o['A'], o['B'], o['gap'], x0 - o['xbar'][:, 0], o['xbar'], o['ubar'],
+                      np.broadcast_to(xref, (B, N + 1, 17)), np.broadcast_to(uref, (B, N, 6)), spec)
+    eb = relerr(U - o['ubar'], dd).max()
+    print(f'17/6 box fp64 {mode}: u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e} vs oracle, {eb:.2e} vs BVLS; '
+          f'{act.mean():.1%} of (k, m) at a bound, oracle iterations max {o["iters"].max()}')
+    assert max(e) <= 1e-9
+    assert eb <= 1e-5

@@ -101,3 +101,25 @@ def test_mpc_solve17_matches_dense_qp(mode):
     assert (o['status'] == 0).all()
     du = _dense_unconstrained(o, xref, uref, spec)
     assert np.abs((o['U'] - o['ubar']) - du).max() <= 1e-8 * max(1.0, np.abs(du).max())
+
+
+def test_ipm_box_matches_dense_bvls_and_kkt():
+    """The interior point of the 17/6 input box (oracle.ocp.ipm_box_solve) against an
+    independent condensed box-QP solve (SciPy BVLS) and the KKT conditions."""
+    from oracle.ocp import dense_box_qp
+    N, B = 10, 4
+    lbu = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])
+    ubu = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+    spec = FullSpec(N=N, lbu=lbu, ubu=ubu)
+    x0, _, p = _random_point(B, 5)
+    x0[:, 3:6] *= 0.5
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2] = 3.5
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    o = mpc_solve17(x0, xref, uref, spec, p)
+    assert (o['status'] == 0).all() and o['iters'].max() < 60
+    du = o['U'] - o['ubar']
+    assert (o['U'] >= lbu - 1e-12).all() and (o['U'] <= ubu + 1e-12).all()
+    dd = dense_box_qp(o['A'], o['B'], o['gap'], np.zeros((B, 17)), o['xbar'], o['ubar'], xref, uref, spec)
+    assert np.abs(du - dd).max() <= 1e-6 * max(1.0, np.abs(dd).max())
