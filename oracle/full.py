@@ -59,6 +59,8 @@ class FullSpec:
     cost_scale: float | None = None       # default dt (acados time_steps)
     lbu: np.ndarray | None = None
     ubu: np.ndarray | None = None
+    lbx: np.ndarray | None = None         # state box on stages 1..N-1 (JSON idxbx), needs lbu
+    ubx: np.ndarray | None = None
     params: Params = field(default_factory=Params)
     max_as_iter: int = 200
 
@@ -162,7 +164,7 @@ def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=N
     dx0 = x0 - xbar[:, 0]
     if spec.boxed:   # interior point (the active set needs thousands of exchanges here)
         dx, du, status, iters = ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec,
-                                              max_iter=spec.max_as_iter)
+                                              max_iter=spec.max_as_iter, lbx=spec.lbx, ubx=spec.ubx)
     else:
         dx, du, _, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
         status = np.where(ok, STATUS_OK, STATUS_QP_FAIL).astype(np.int32)

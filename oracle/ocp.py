@@ -123,11 +123,11 @@ def _masked_stage(Huu, Hux, hu, fixed, delta):
 
 
 def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
-                  fixed=None, delta=None, Rd=None, rd=None):
+                  fixed=None, delta=None, Rd=None, rd=None, Qd=None, qd=None):
     """Solve the (masked) LQ QP.  Returns dx (B,N+1,nx), du (B,N,nu), mu (B,N,nu), ok (B,).
     Dimensions come from A (nx) and Bm (nu): the 12/4 slice and the 17/6 model share it.
-    Rd, rd (B,N,nu): extra diagonal input Hessian and input gradient per stage (the barrier
-    terms of ``ipm_box_solve``)."""
+    Rd, rd (B,N,nu) / Qd, qd (B,N,nx): extra diagonal input / state Hessian and gradient per
+    stage k < N (the barrier terms of ``ipm_box_solve``)."""
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
     s = spec.s
@@ -153,15 +153,25 @@ def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
         if Rd is not None:
             Huu = Huu + Rd[:, k, :, None] * np.eye(NU)[None]
             hu = hu + rd[:, k]
+        if Qd is not None:
+            Hxx = Hxx + Qd[:, k, :, None] * np.eye(NX)[None]
+            hx = hx + qd[:, k]
         fk = None if fixed is None else fixed[:, k]
         dk = None if delta is None else delta[:, k]
         Ht, Hxt, ht = _masked_stage(Huu, Hux, hu, fk, dk)
         try:
             L = np.linalg.cholesky(Ht)
-        except np.linalg.LinAlgError:
-            ev_ok = np.all(np.linalg.eigvalsh(Ht) > 0, axis=-1)
+        except np.linalg.LinAlgError:   # rare: find the failing instances one by one
+            ev_ok = np.ones(Bsz, dtype=bool)
+            for b in range(Bsz):
+                try:
+                    np.linalg.cholesky(Ht[b])
+                except np.linalg.LinAlgError:
+                    ev_ok[b] = False
             ok &= ev_ok
             Ht = np.where(ev_ok[:, None, None], Ht, np.eye(NU)[None])
+            Hxt = np.where(ev_ok[:, None, None], Hxt, 0.0)
+            ht = np.where(ev_ok[:, None], ht, 0.0)
             L = np.linalg.cholesky(Ht)
         Kk = -np.linalg.solve(Ht, Hxt)
         kk = -np.linalg.solve(Ht, ht[..., None])[..., 0]
@@ -245,66 +255,125 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     return out_dx, out_du, status, iters
 
 
-IPM_SIGMA, IPM_TAU, IPM_THETA, IPM_TOL = 0.1, 0.995, 0.1, 1e-12
+IPM_SIGMA, IPM_TAU, IPM_THETA, IPM_TOL = 0.1, 0.995, 0.1, 1e-10
 
 
-def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60):
-    """Input-box QP by a primal-dual interior point over the Riccati recursion (the method of
-    acados' HPIPM; used for the full 17/6 model, where the active set above can need thousands
-    of exchanges).  Iterate (du, dx, lambda_l, lambda_u) with du strictly inside
-    [lb, ub] = [lbu - ubar, ubu - ubar] and dx consistent with the dynamics.  Every iteration
-    takes the Newton step of the barrier-perturbed KKT system: the LQ problem in the step
+def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lbx=None, ubx=None):
+    """Box-constrained QP by a primal-dual interior point over the Riccati recursion (the method
+    of acados' HPIPM; the full 17/6 model, where the active set above can need thousands of
+    exchanges).  Constraint rows: the input box on stages 0..N-1 and, when ``lbx``/``ubx`` are
+    given (JSON idxbx), the state box on stages 1..N-1.  Each row y in [lb, ub] carries slacks
+    s_l, s_u > 0 with residuals r_l = y - lb - s_l, r_u = ub - y - s_u (an infeasible start: the
+    state rows need not be feasible initially) and multipliers lambda_l, lambda_u > 0.  Every
+    iteration takes the Newton step of the barrier-perturbed KKT system: the LQ problem in
     (Delta x, Delta u) LINEARISED AT THE CURRENT ITERATE (references shifted by (dx, du), zero
-    gaps, Delta x_0 = 0 — so the step never comes out of a difference of large numbers when
-    D = lambda_l/s_l + lambda_u/s_u grows at active bounds) with input Hessian + D and input
-    gradient - sigma mu (1/s_l - 1/s_u); then a fraction tau of the way to the boundary in the
-    primal and dual variables (common length).  Start: du = clip(0, lb + theta w, ub - theta w)
-    (dx by the dynamics), lambda = 1.  Stops when mu = mean(lambda s) <= IPM_TOL or after
+    gaps, Delta x_0 = 0) with Hessian + D and gradient + d per row,
+        D = lambda_l/s_l + lambda_u/s_u,
+        d = -sigma mu (1/s_l - 1/s_u) + (lambda_l/s_l) r_l - (lambda_u/s_u) r_u,
+    then a common step, a fraction tau of the way to the boundary of (s, lambda).  Start: du =
+    clip(0, lb + theta w, ub - theta w) (dx by the dynamics), s = max(distance, theta w),
+    lambda = 1.  Stops when mu = mean(lambda s) <= IPM_TOL and max |r| <= 1e-9, or after
     ``max_iter`` iterations.  Returns dx, du, status, iterations."""
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
-    lb = np.asarray(spec.lbu, dtype=np.float64) - ubar
-    ub = np.asarray(spec.ubu, dtype=np.float64) - ubar
-    w = ub - lb
-    du = np.clip(np.zeros_like(lb), lb + IPM_THETA * w, ub - IPM_THETA * w)
+    lbu = np.asarray(spec.lbu, dtype=np.float64) - ubar      # input rows, du coordinates
+    ubu = np.asarray(spec.ubu, dtype=np.float64) - ubar
+    wu = ubu - lbu
+    du = np.clip(np.zeros_like(lbu), lbu + IPM_THETA * wu, ubu - IPM_THETA * wu)
     dx = np.empty((Bsz, N + 1, NX))
     dx[:, 0] = dx0
     for k in range(N):
         dx[:, k + 1] = np.einsum('bij,bj->bi', A[:, k], dx[:, k]) + np.einsum('bij,bj->bi', Bm[:, k], du[:, k]) + gap[:, k]
-    ll = np.ones_like(du)
-    lu = np.ones_like(du)
+    sx = lbx is not None
+    if sx:   # state rows on stages 1..N-1 (dx coordinates; stage 0 is pinned, no terminal box)
+        lbx_ = np.asarray(lbx, dtype=np.float64) - xbar[:, 1:N]
+        ubx_ = np.asarray(ubx, dtype=np.float64) - xbar[:, 1:N]
+        wx = ubx_ - lbx_
+    rows = N * NU + (N - 1) * NX * sx
+
+    def slacks_init(y, lb, ub, w):
+        return np.maximum(y - lb, IPM_THETA * w), np.maximum(ub - y, IPM_THETA * w)
+
+    sul, suu = du - lbu, ubu - du
+    llu, luu = np.ones_like(du), np.ones_like(du)
+    if sx:
+        sxl, sxu = slacks_init(dx[:, 1:N], lbx_, ubx_, wx)
+        llx, lux = np.ones_like(sxl), np.ones_like(sxl)
     it = np.zeros(Bsz, dtype=np.int32)
     ok = np.ones(Bsz, dtype=bool)
     act = np.ones(Bsz, dtype=bool)
     zgap = np.zeros_like(gap)
     zdx0 = np.zeros_like(dx0)
+
+    def measure():
+        tot = (llu * sul + luu * suu).sum(axis=(1, 2))
+        res = np.maximum(np.abs(du - lbu - sul).max(axis=(1, 2)), np.abs(ubu - du - suu).max(axis=(1, 2)))
+        if sx:
+            tot = tot + (llx * sxl + lux * sxu).sum(axis=(1, 2))
+            yx = dx[:, 1:N]
+            res = np.maximum(res, np.maximum(np.abs(yx - lbx_ - sxl).max(axis=(1, 2)),
+                                             np.abs(ubx_ - yx - sxu).max(axis=(1, 2))))
+        return tot / (2 * rows), res
+
+    def newton(y, lb, ub, sl, su, ll, lu, smu):
+        rl, ru = y - lb - sl, ub - y - su
+        D = ll / sl + lu / su
+        d = -smu * (1.0 / sl - 1.0 / su) + (ll / sl) * rl - (lu / su) * ru
+        return D, d, rl, ru
+
+    def duals(dy, rl, ru, sl, su, ll, lu, smu):
+        dsl, dsu = dy + rl, ru - dy
+        dll = (smu - ll * sl - ll * dsl) / sl
+        dlu = (smu - lu * su - lu * dsu) / su
+        return dsl, dsu, dll, dlu
+
+    def maxstep(v, dv):
+        with np.errstate(divide='ignore', invalid='ignore'):
+            return np.where(dv < 0, -v / dv, np.inf).min(axis=(1, 2))
+
     for _ in range(max_iter):
-        sl, su = du - lb, ub - du
-        mu = (ll * sl + lu * su).sum(axis=(1, 2)) / (2 * N * NU)
-        act = act & (mu > IPM_TOL)
+        mu, res = measure()
+        act = act & ((mu > IPM_TOL) | (res > 1e-9))
         if not act.any():
             break
         smu = (IPM_SIGMA * mu)[:, None, None]
-        D = ll / sl + lu / su
-        d = -smu * (1.0 / sl - 1.0 / su)
-        ddx, dd, _, ok2 = riccati_solve(A, Bm, zgap, zdx0, xbar + dx, ubar + du, xref, uref, spec, Rd=D, rd=d)
+        Du, du_lin, rul, ruu = newton(du, lbu, ubu, sul, suu, llu, luu, smu)
+        Qd = qd = None
+        if sx:
+            Dx, dx_lin, rxl, rxu = newton(dx[:, 1:N], lbx_, ubx_, sxl, sxu, llx, lux, smu)
+            Qd = np.zeros((Bsz, N, NX))
+            qd = np.zeros((Bsz, N, NX))
+            Qd[:, 1:N], qd[:, 1:N] = Dx, dx_lin
+        # an instance whose iterate left the finite range (an infeasible QP drives the multipliers
+        # to infinity) is frozen: it keeps a harmless system and fails at the end
+        fin = np.isfinite(Du).all(axis=(1, 2)) & np.isfinite(du_lin).all(axis=(1, 2)) & np.isfinite(dx).all(axis=(1, 2))
+        if sx:
+            fin &= np.isfinite(Qd).all(axis=(1, 2)) & np.isfinite(qd).all(axis=(1, 2))
+        ok &= fin
+        act &= fin
+        f3 = fin[:, None, None]
+        Du, du_lin = np.where(f3, Du, 1.0), np.where(f3, du_lin, 0.0)
+        if sx:
+            Qd, qd = np.where(f3, Qd, 1.0), np.where(f3, qd, 0.0)
+        ddx, dd, _, ok2 = riccati_solve(A, Bm, zgap, zdx0, xbar + np.where(f3, dx, 0.0), ubar + np.where(f3, du, 0.0),
+                                        xref, uref, spec, Rd=Du, rd=du_lin, Qd=Qd, qd=qd)
         ok &= ok2 | ~act
-        dll = (smu - ll * sl - ll * dd) / sl
-        dlu = (smu - lu * su + lu * dd) / su
-        with np.errstate(divide='ignore', invalid='ignore'):
-            ap = np.where(dd < 0, -sl / dd, np.where(dd > 0, su / dd, np.inf)).min(axis=(1, 2))
-            ad = np.minimum(np.where(dll < 0, -ll / dll, np.inf).min(axis=(1, 2)),
-                            np.where(dlu < 0, -lu / dlu, np.inf).min(axis=(1, 2)))
-        alpha = np.minimum(1.0, IPM_TAU * np.minimum(ap, ad))
+        steps = []
+        dul = duals(dd, rul, ruu, sul, suu, llu, luu, smu)
+        steps += [maxstep(v, dv) for v, dv in zip((sul, suu, llu, luu), dul)]
+        if sx:
+            dxl = duals(ddx[:, 1:N], rxl, rxu, sxl, sxu, llx, lux, smu)
+            steps += [maxstep(v, dv) for v, dv in zip((sxl, sxu, llx, lux), dxl)]
+        alpha = np.minimum(1.0, IPM_TAU * np.min(np.stack(steps), axis=0))
         alpha = np.where(act, alpha, 0.0)[:, None, None]
         du = du + alpha * dd
         dx = dx + alpha * ddx
-        ll = ll + alpha * dll
-        lu = lu + alpha * dlu
+        sul, suu, llu, luu = (v + alpha * dv for v, dv in zip((sul, suu, llu, luu), dul))
+        if sx:
+            sxl, sxu, llx, lux = (v + alpha * dv for v, dv in zip((sxl, sxu, llx, lux), dxl))
         it += act
-    sl, su = du - lb, ub - du
-    mu = (ll * sl + lu * su).sum(axis=(1, 2)) / (2 * N * NU)
-    status = np.where(mu <= IPM_TOL, STATUS_OK, STATUS_MAXITER).astype(np.int32)
+    mu, res = measure()
+    status = np.where((mu <= IPM_TOL) & (res <= 1e-9), STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
     return dx, du, status, it
 
@@ -389,3 +458,62 @@ def dense_box_qp(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
                          max_iter=10000)
         out_du[b] = res.x.reshape(N, NU)
     return out_du
+
+
+def dense_kkt_polish(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, du, lbx=None, ubx=None, act_tol=1e-6):
+    """Independent check (tests only) of a box-QP solution with state rows: condense the QP in du,
+    take the rows within ``act_tol`` of a bound in the given ``du`` as the active set, solve the
+    equality-constrained QP on it exactly (dense KKT system) and test the KKT conditions (primal
+    feasibility, multiplier signs).  Returns (du_polished [B,N,NU], kkt_ok [B], min multiplier [B],
+    max violation [B])."""
+    Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
+    s = spec.s
+    Q, R, QN = (np.asarray(M, dtype=np.float64) for M in (spec.Q, spec.R, spec.QN))
+    nz = N * NU
+    out = np.empty((Bsz, N, NU))
+    ok = np.zeros(Bsz, dtype=bool)
+    lmin = np.zeros(Bsz)
+    viol = np.zeros(Bsz)
+    for b in range(Bsz):
+        c = np.zeros((N + 1, NX))
+        G = np.zeros((N + 1, NX, nz))
+        c[0] = dx0[b]
+        for k in range(N):
+            c[k + 1] = A[b, k] @ c[k] + gap[b, k]
+            G[k + 1] = A[b, k] @ G[k]
+            G[k + 1][:, k * NU:(k + 1) * NU] += Bm[b, k]
+        H = np.zeros((nz, nz))
+        g = np.zeros(nz)
+        for k in range(N + 1):
+            W = QN if k == N else s * Q
+            e = c[k] + xbar[b, k] - xref[b, k]
+            H += G[k].T @ W @ G[k]
+            g += G[k].T @ W @ e
+        for k in range(N):
+            sl = slice(k * NU, (k + 1) * NU)
+            H[sl, sl] += s * R
+            g[sl] += s * R @ (ubar[b, k] - uref[b, k])
+        # rows C z <= h: input box, then state box on stages 1..N-1
+        C = [np.eye(nz), -np.eye(nz)]
+        h = [np.tile(np.asarray(spec.ubu, dtype=np.float64), N) - ubar[b].reshape(-1),
+             -(np.tile(np.asarray(spec.lbu, dtype=np.float64), N) - ubar[b].reshape(-1))]
+        if lbx is not None:
+            Gx = G[1:N].reshape(-1, nz)
+            cx = (c[1:N] + xbar[b, 1:N]).reshape(-1)
+            C += [Gx, -Gx]
+            h += [np.tile(np.asarray(ubx, dtype=np.float64), N - 1) - cx,
+                  -(np.tile(np.asarray(lbx, dtype=np.float64), N - 1) - cx)]
+        C = np.vstack(C)
+        h = np.concatenate(h)
+        z = du[b].reshape(-1)
+        act = np.nonzero(C @ z - h > -act_tol)[0]
+        Ca = C[act]
+        K = np.block([[H, Ca.T], [Ca, np.zeros((len(act), len(act)))]])
+        sol = np.linalg.lstsq(K, np.concatenate([-g, h[act]]), rcond=None)[0]
+        zp, lam = sol[:nz], sol[nz:]
+        out[b] = zp.reshape(N, NU)
+        lmin[b] = lam.min() if len(lam) else 0.0
+        viol[b] = max(0.0, (C @ zp - h).max())
+        ok[b] = lmin[b] >= -1e-7 and viol[b] <= 1e-9
+    return out, ok, lmin, viol

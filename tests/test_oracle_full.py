@@ -123,3 +123,38 @@ def test_ipm_box_matches_dense_bvls_and_kkt():
     assert (o['U'] >= lbu - 1e-12).all() and (o['U'] <= ubu + 1e-12).all()
     dd = dense_box_qp(o['A'], o['B'], o['gap'], np.zeros((B, 17)), o['xbar'], o['ubar'], xref, uref, spec)
     assert np.abs(du - dd).max() <= 1e-6 * max(1.0, np.abs(dd).max())
+
+
+def test_ipm_state_box_kkt():
+    """The reference's state box (acados_ocp_blasterModel.json idxbx/lbx/ubx, stages 1..N-1) on
+    top of the input box: the interior point's solution satisfies the KKT conditions of the
+    condensed QP (active set taken from the solution and solved exactly, multipliers >= 0), and
+    the state box is active on a good share of the rows."""
+    import json
+
+    from oracle.ocp import dense_kkt_polish
+    d = json.load(open(os.path.join(GOLD, 'ocp_json_pin.json')))
+    lbx, ubx = np.array(d['lbx']), np.array(d['ubx'])
+    N, B = 20, 6
+    spec = FullSpec(N=N, lbu=np.array(d['lbu']), ubu=np.array(d['ubu']), lbx=lbx, ubx=ubx)
+    rng = np.random.default_rng(31)
+    x0 = rng.uniform(0.25 * lbx, 0.25 * ubx, (B, 17))
+    x0[:, 2] = 3.5 + rng.uniform(-0.5, 0.5, B)
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2] = 3.5
+    xref[..., 14] = 0.2
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    p = np.tile(default_p25(), (B, 1))
+    p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
+    o = mpc_solve17(x0, xref, uref, spec, p)
+    assert (o['status'] == 0).all() and o['iters'].max() < 60
+    X = o['X'][:, 1:N]
+    assert (X >= lbx - 1e-9).all() and (X <= ubx + 1e-9).all()
+    n_act = ((X - lbx < 1e-6) | (ubx - X < 1e-6)).sum()
+    assert n_act >= B * 10
+    du = o['U'] - o['ubar']
+    dp, ok, lmin, viol = dense_kkt_polish(o['A'], o['B'], o['gap'], np.zeros((B, 17)), o['xbar'], o['ubar'],
+                                          xref, uref, spec, du, lbx=lbx, ubx=ubx)
+    assert ok.all(), (lmin, viol)
+    assert np.abs(du - dp).max() <= 1e-5 * max(1.0, np.abs(dp).max())
