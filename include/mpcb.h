@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MPCB_ABI_VERSION 2
+#define MPCB_ABI_VERSION 3
 
 enum { MPCB_F64 = 0, MPCB_F32 = 1 };
 enum { MPCB_MODE_ROLLOUT = 0, MPCB_MODE_ITERATE = 1 };
@@ -57,8 +57,10 @@ typedef struct mpcb_config {
   int32_t N;             /* horizon (ocp.dims.N, blastermodel.py:226) */
   int32_t dtype;         /* MPCB_F64 | MPCB_F32 */
   int32_t box_u;         /* 1: lbu <= u <= ubu on stages 0..N-1 (idxbu, blastermodel.py:261) */
-  int32_t max_as_iter;   /* active-set iteration cap for box_u */
-  int32_t reserved[2];
+  int32_t max_as_iter;   /* active-set / interior-point iteration cap for box_u */
+  int32_t box_x;         /* 17/6 only, needs box_u: lbx <= x_k <= ubx on stages 1..N-1 (idxbx,
+                            blastermodel.py:255-258 statesBound; JSON constraints.lbx/ubx) */
+  int32_t reserved;
   double dt;             /* Tf / N (solver_options.tf, blastermodel.py:287) */
   double cost_scale;     /* stage-cost scaling; acados uses time_steps[k] = dt */
   double mass, lx, ly, c, g, t_blast;   /* 17/6: t_blast is the default parameter p[24] */
@@ -67,6 +69,7 @@ typedef struct mpcb_config {
   double R[MPCB_MAX_NU * MPCB_MAX_NU];   /* stage input weight  (W[nx:,nx:]) */
   double QN[MPCB_MAX_NX * MPCB_MAX_NX];  /* terminal weight (W_e = Q_t) */
   double lbu[MPCB_MAX_NU], ubu[MPCB_MAX_NU];
+  double lbx[MPCB_MAX_NX], ubx[MPCB_MAX_NX];   /* state box (box_x) */
 } mpcb_config;
 
 typedef struct mpcb_handle mpcb_handle;

@@ -28,7 +28,7 @@ class MpcbConfig(ctypes.Structure):
     _fields_ = [
         ('nx', ctypes.c_int32), ('nu', ctypes.c_int32), ('N', ctypes.c_int32),
         ('dtype', ctypes.c_int32), ('box_u', ctypes.c_int32), ('max_as_iter', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 2),
+        ('box_x', ctypes.c_int32), ('reserved', ctypes.c_int32),
         ('dt', ctypes.c_double), ('cost_scale', ctypes.c_double),
         ('mass', ctypes.c_double), ('lx', ctypes.c_double), ('ly', ctypes.c_double),
         ('c', ctypes.c_double), ('g', ctypes.c_double), ('t_blast', ctypes.c_double),
@@ -37,6 +37,7 @@ class MpcbConfig(ctypes.Structure):
         ('R', ctypes.c_double * (MPCB_MAX_NU * MPCB_MAX_NU)),
         ('QN', ctypes.c_double * (MPCB_MAX_NX * MPCB_MAX_NX)),
         ('lbu', ctypes.c_double * MPCB_MAX_NU), ('ubu', ctypes.c_double * MPCB_MAX_NU),
+        ('lbx', ctypes.c_double * MPCB_MAX_NX), ('ubx', ctypes.c_double * MPCB_MAX_NX),
     ]
 
 

@@ -15,7 +15,9 @@ parts this build implements onto ``MPCConfig``:
 
 The physical constants (mass, J, l_x, l_y, c) are baked into the CasADi expressions, not the
 JSON: they are keyword arguments with the reference's defaults (simulation_blaster.py:12-21).
-State boxes (``idxbx``, stages 1..N-1) are returned in ``info`` and reported as not applied.
+The state box (``idxbx``/``lbx``/``ubx``, stages 1..N-1) is applied on the 17/6 model when it covers
+every state (the reference's idxbx = range(nx)); otherwise, and on the 12/4 slice, it is returned
+in ``info`` and reported as not applied.
 """
 from __future__ import annotations
 
@@ -39,7 +41,7 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     """Returns (MPCConfig, info) for a JSON path or an already-parsed dict.
 
     info: yref [ny] and yref_e [ny_e] (the JSON's stage / terminal references), p [np],
-    idxbx / lbx / ubx (not applied by the device), and ``dropped`` (what was not mapped)."""
+    idxbx / lbx / ubx (as in the JSON), and ``dropped`` (what was not mapped)."""
     d = json.load(open(src)) if isinstance(src, str) else src
     dims = d['dims']
     nx, nu, N = int(dims['nx']), int(dims['nu']), int(dims['N'])
@@ -92,8 +94,18 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     t_blast = float(p[24]) if p.size >= 25 else 0.0
     dropped = []
     idxbx = list(np.atleast_1d(con.get('idxbx', [])).astype(int))
+    lbx = ubx = None
     if idxbx:
-        dropped.append('state box idxbx (stages 1..N-1)')
+        # the device's state box covers every state (the reference sets idxbx = range(nx),
+        # blastermodel.py:267) of the 17/6 model, together with the input box
+        if (not slice_12_4 and nx == NX17 and sorted(idxbx) == list(range(nx)) and lbu is not None
+                and np.isfinite(con['lbx']).all() and np.isfinite(con['ubx']).all()):
+            lbx = np.empty(nx)
+            ubx = np.empty(nx)
+            lbx[idxbx] = np.asarray(con['lbx'], dtype=np.float64)
+            ubx[idxbx] = np.asarray(con['ubx'], dtype=np.float64)
+        else:
+            dropped.append('state box idxbx (stages 1..N-1)')
 
     if slice_12_4 and nx == NX17:
         Q, R, We = Q[:NX, :NX], R[:NU, :NU], We[:NX, :NX]
@@ -104,7 +116,7 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     phys = dict(mass=9.0, J=np.diag([0.50781, 0.47314, 0.72975]), lx=0.3434, ly=0.3475, c=0.03)
     phys.update(physical)
     cfg = MPCConfig(N=N, dt=dt, dtype=dtype, Q=Q, R=R, QN=We, cost_scale=dt, lbu=lbu, ubu=ubu,
-                    t_blast=t_blast, nx=nx, nu=nu, **phys)
+                    lbx=lbx, ubx=ubx, t_blast=t_blast, nx=nx, nu=nu, **phys)
     for what in dropped:
         warnings.warn(f'acados JSON: {what} not applied by the device path', stacklevel=2)
     info = dict(yref=np.asarray(cost.get('yref', np.zeros(ny)), dtype=np.float64),

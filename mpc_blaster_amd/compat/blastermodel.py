@@ -3,11 +3,11 @@
 Same signature and call sequence as the reference:
 ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
 controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
-``full_model=True`` keeps the reference's 17/6 model, its weights and its input box
-(controlBound: thrusts and swivel rates) unchanged — the device's 17/6 path.  The default keeps the
-12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4], thrust bounds
-controlBound[:, :4].  State bounds (statesBound) are accepted but not enforced (stage boxes are
-not part of the build; the reference scripts only pin x0).
+``full_model=True`` keeps the reference's 17/6 model, its weights, its input box (controlBound:
+thrusts and swivel rates) and its state box (statesBound, stages 1..N-1, blastermodel.py:267-269)
+unchanged — the device's 17/6 path; a statesBound with non-finite entries leaves the state box
+off.  The default keeps the 12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4],
+thrust bounds controlBound[:, :4]; there statesBound is accepted but not enforced.
 """
 from __future__ import annotations
 
@@ -40,6 +40,13 @@ class blasterModel:  # noqa: N801  (reference class name)
         self._full = bool(full_model)
         self._cfg = None
 
+    def _state_box(self):
+        """statesBound as the 17/6 state box (needs the input box too, as the device does)."""
+        sb = self._statesBound
+        if sb.shape == (2, NX17) and np.isfinite(sb).all() and self._controlBound.size > 0:
+            return dict(lbx=sb[0].copy(), ubx=sb[1].copy())
+        return {}
+
     def generateModel(self):
         """Builds the problem definition (the dynamics themselves live in the HIP kernels)."""
         cb = self._controlBound
@@ -52,7 +59,8 @@ class blasterModel:  # noqa: N801  (reference class name)
                 Q=self._Q_weight[:NX17, :NX17], R=self._R_weight[:NU17, :NU17],
                 QN=self._Q_weight_t[:NX17, :NX17], t_blast=self._blastThruster * 9.81,
                 nx=NX17, nu=NU17,
-                lbu=cb[0][:NU17] if cb.size else None, ubu=cb[1][:NU17] if cb.size else None)
+                lbu=cb[0][:NU17] if cb.size else None, ubu=cb[1][:NU17] if cb.size else None,
+                **self._state_box())
             return 0
         self._cfg = MPCConfig(
             N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
@@ -67,7 +75,8 @@ class blasterModel:  # noqa: N801  (reference class name)
     def generateController(self):
         if self._cfg is None:
             self.generateModel()
-        if self._statesBound.size and np.isfinite(self._statesBound).any():
+        if not (self._full and self._cfg.lbx is not None) and self._statesBound.size and \
+                np.isfinite(self._statesBound).any():
             warnings.warn('statesBound is not enforced by this build (stage state boxes are out of '
                           'scope); x0 is pinned through set(0, "lbx"/"ubx")', stacklevel=2)
         ocp = AcadosOcpSolver(self._cfg, batch=self._batch, device=self._device,

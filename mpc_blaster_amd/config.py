@@ -52,6 +52,8 @@ class MPCConfig:
     cost_scale: float | None = None    # default dt
     lbu: np.ndarray | None = None      # None -> no input box
     ubu: np.ndarray | None = None
+    lbx: np.ndarray | None = None      # 17/6 state box on stages 1..N-1 (needs lbu/ubu)
+    ubx: np.ndarray | None = None
     max_as_iter: int = 200
     nx: int = NX
     nu: int = NU
@@ -70,13 +72,18 @@ class MPCConfig:
             raise ValueError(f'dtype {self.dtype!r}')
         if (self.lbu is None) != (self.ubu is None):
             raise ValueError('lbu and ubu must be given together')
+        if (self.lbx is None) != (self.ubx is None):
+            raise ValueError('lbx and ubx must be given together')
+        if self.lbx is not None and (nx != NX17 or self.lbu is None):
+            raise ValueError('the state box is implemented for the 17/6 model together with the input box')
 
     @classmethod
     def full(cls, **kw) -> 'MPCConfig':
         """The reference's own OCP (acados_ocp_blasterModel.json, simulation_blaster.py:12-30):
         17/6 model, N = 60, Tf = 2 (dt = 1/30), T_blast = 2.2 * 9.81, W = diag(Q17, R6),
         W_e = 10 Q17.  Pass ``lbu``/``ubu`` for the reference's input box (JSON idxbu: thrusts
-        [0, 65] N, swivel rates +-0.0873 rad/s); state boxes are not applied."""
+        [0, 65] N, swivel rates +-0.0873 rad/s) and ``lbx``/``ubx`` for its state box (JSON idxbx,
+        stages 1..N-1)."""
         d = dict(N=60, dt=2.0 / 60.0, t_blast=2.2 * 9.81, nx=NX17, nu=NU17)
         d.update(kw)
         return cls(**d)
@@ -112,6 +119,12 @@ class MPCConfig:
             ub = np.broadcast_to(np.asarray(self.ubu, dtype=np.float64), (self.nu,))
             for i in range(self.nu):
                 c.lbu[i], c.ubu[i] = float(lb[i]), float(ub[i])
+        if self.lbx is not None:
+            c.box_x = 1
+            lb = np.broadcast_to(np.asarray(self.lbx, dtype=np.float64), (self.nx,))
+            ub = np.broadcast_to(np.asarray(self.ubx, dtype=np.float64), (self.nx,))
+            for i in range(self.nx):
+                c.lbx[i], c.ubx[i] = float(lb[i]), float(ub[i])
         return c
 
     @property

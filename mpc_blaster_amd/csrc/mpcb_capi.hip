@@ -112,6 +112,10 @@ static void fill_weights17(const mpcb_config& c, Weights17<T>& w) {
     w.lbu[i] = (T)c.lbu[i];
     w.ubu[i] = (T)c.ubu[i];
   }
+  for (int i = 0; i < NX17; ++i) {
+    w.lbx[i] = (T)c.lbx[i];
+    w.ubx[i] = (T)c.ubx[i];
+  }
   // acados parameter_values default: every Jacobian block 0, T_blast from the config
   for (int i = 0; i < NP17; ++i) w.p[i] = T(0);
   w.p[24] = (T)c.t_blast;
@@ -142,6 +146,12 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     for (int m = 0; m < NU17; ++m)
       if (!(cfg->ubu[m] > cfg->lbu[m]))
         return fail(MPCB_E_INVALID, "17/6 input box needs lbu < ubu (component %d)", m);
+  if (cfg->box_x && !(full && cfg->box_u))
+    return fail(MPCB_E_UNSUPPORTED, "box_x is implemented for the 17/6 model together with box_u");
+  if (cfg->box_x)
+    for (int i = 0; i < NX17; ++i)
+      if (!(cfg->ubx[i] > cfg->lbx[i]))
+        return fail(MPCB_E_INVALID, "17/6 state box needs lbx < ubx (component %d)", i);
   if (cfg->N < 1 || cfg->N > 4096) return fail(MPCB_E_INVALID, "horizon N=%d out of range", cfg->N);
   if (!full && cfg->box_u && cfg->N > 64) return fail(MPCB_E_UNSUPPORTED, "box_u needs N <= 64 (N=%d)", cfg->N);
   if (cfg->dtype != MPCB_F64 && cfg->dtype != MPCB_F32)
@@ -297,6 +307,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
     a.ws = (T*)h->scratch;
     a.box = h->cfg.box_u;
+    a.sbox = h->cfg.box_x;
     a.max_as_iter = h->cfg.max_as_iter;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       a.b0 = b0;

@@ -191,6 +191,7 @@ struct Weights17 {
   T R[NU17 * NU17];
   T QN[NX17 * NX17];
   T lbu[NU17], ubu[NU17];
+  T lbx[NX17], ubx[NX17];   // state box on stages 1..N-1 (FullArgs::sbox)
   T p[NP17];
 };
 
@@ -209,14 +210,15 @@ struct FullArgs {
   T* u0; T* X; T* U; int32_t* status;
   T* ws;             // chunk workspace: per instance full17_elems(N) elements
   int box;           // input box lbu <= u <= ubu (interior-point iterations)
+  int sbox;          // with box: state box lbx <= x_k <= ubx on stages 1..N-1
   int max_as_iter;   // iteration cap
 };
 
 __host__ __device__ constexpr int64_t full17_elems(int N) {
   // XB (N+1)x17 | UB Nx6 | AB N x 23 columns x 17 | KR N x (6x17 + 6) | GP N x 17 |
-  // input box: DX, DDX (N+1)x17 | IP N x 18 | DDU N x 6
+  // boxes: DX, DDX (N+1)x17 | IP N x 18 | DDU N x 6 | IX (N+1) x 4 x 17
   return (int64_t)(N + 1) * NX17 + (int64_t)N * (NU17 + NZ17 * NX17 + NU17 * NX17 + NU17 + NX17) +
-         2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17);
+         2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17) + 4 * (int64_t)(N + 1) * NX17;
 }
 
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st);

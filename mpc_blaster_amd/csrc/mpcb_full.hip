@@ -83,7 +83,7 @@ template <class T> __device__ __forceinline__ T sel17(const T* x, int i) {
 template <class T>
 struct Ws17 {
   T *XB, *UB, *AB, *KR, *GP;
-  T *DX, *DDX, *IP, *DDU;
+  T *DX, *DDX, *IP, *DDU, *IX;
   static constexpr int KR_N = NU17 * NX17 + NU17;
   __device__ __forceinline__ Ws17(T* ws, int N) {
     XB = ws;                                     // [N+1][17] nominal states
@@ -96,6 +96,8 @@ struct Ws17 {
     DDX = DX + (int64_t)(N + 1) * NX17;          // [N+1][17]
     IP = DDX + (int64_t)(N + 1) * NX17;          // [N][18]: du | lambda_l | lambda_u
     DDU = IP + (int64_t)N * 18;                  // [N][6]
+    // state box: slacks and multipliers s_l | s_u | lambda_l | lambda_u of the rows of stage k
+    IX = DDU + (int64_t)N * NU17;                // [N+1][4][17]
   }
 };
 
@@ -215,6 +217,28 @@ struct R17 {
   bool dir, valid;
 };
 
+// One state-box row (stage k, state lane j): dx-coordinate bounds, the iterate y = dx_k[j], its
+// slacks / multipliers and the residuals r_l = y - lb - s_l, r_u = ub - y - s_u (the state rows
+// start infeasible: oracle.ocp.ipm_box_solve).
+template <class T>
+struct SRow17 {
+  T y, lb, ub, sl, su, ll, lu, rl, ru;
+  __device__ __forceinline__ SRow17(const R17<T>& r, int k) {
+    const int j = r.j;
+    const T xb = r.w.XB[(int64_t)k * NX17 + j];
+    y = r.w.DX[(int64_t)k * NX17 + j];
+    lb = r.a.W->lbx[j] - xb;
+    ub = r.a.W->ubx[j] - xb;
+    const T* ix = r.w.IX + (int64_t)k * 4 * NX17 + j;
+    sl = ix[0];
+    su = ix[NX17];
+    ll = ix[2 * NX17];
+    lu = ix[3 * NX17];
+    rl = y - lb - sl;
+    ru = ub - y - su;
+  }
+};
+
 template <class T, bool IPM>
 __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
   FullLds<T>& L = r.L;
@@ -283,6 +307,15 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
       G[i] = acc + wgt;
       hj += wgt * L.v[i];
       if (i % 2 == 1) wave_lds_sync();
+    }
+    if constexpr (IPM) {   // state-box rows of this stage: barrier terms on the state lane's diagonal
+      if (r.a.sbox && j < NX17 && k > 0) {
+        const SRow17<T> sr(r, k);
+        const T Dj = sr.ll / sr.sl + sr.lu / sr.su;
+        hj += -smu * (T(1) / sr.sl - T(1) / sr.su) + (sr.ll / sr.sl) * sr.rl - (sr.lu / sr.su) * sr.ru;
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) G[i] += (i == j) ? Dj : T(0);
+      }
     }
 #pragma unroll
     for (int m = 0; m < NU17; ++m) L.Hu[j * NU17 + m] = G[NX17 + m];
@@ -405,15 +438,20 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
   return fin;
 }
 
-constexpr double IPM17_SIGMA = 0.1, IPM17_TAU = 0.995, IPM17_THETA = 0.1, IPM17_TOL = 1e-12;
+constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
+constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6;
 
 // BOX: the input box lbu <= u <= ubu of the reference OCP (blastermodel.py:259-264; thrust
 // [0, 65] N, swivel rate +-0.0873 rad/s) by a primal-dual interior point over the Riccati
-// recursion (acados uses HPIPM's; oracle.ocp.ipm_box_solve is the same iteration): Newton steps
+// recursion (acados uses HPIPM's; oracle.ocp.ipm_box_solve is the same iteration, incl. the
+// adaptive centring sigma = clip(1 - previous step, 0.05, 0.9) and the stall test): Newton steps
 // of the barrier-perturbed KKT system linearised at the current iterate (input Hessian + D,
 // gradient - sigma mu (1/s_l - 1/s_u)), a common primal/dual step length tau to the boundary,
-// until mu = mean(lambda s) <= 1e-12.  (The exact active set of the 12/4 path needs thousands of
-// exchanges on this model: the swivel-rate weight is 1e-5.)
+// until mu = mean(lambda s) <= 1e-12 (or a breakdown of the Newton system once mu <= 1e-8).  (The exact active set of the 12/4 path needs thousands of
+// exchanges on this model: the swivel-rate weight is 1e-5.)  With a.sbox also the state box
+// lbx <= x_k <= ubx on stages 1..N-1 (blastermodel.py:255-258): explicit slacks and multipliers
+// per row (workspace IX, owned by the state lane), an infeasible start, barrier terms on the
+// diagonal of H_xx, and convergence also needs max |r| <= 1e-9.
 template <class T, bool BOX>
 __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
   __shared__ FullLds<T> lds_all[G17];
@@ -465,8 +503,23 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     }
     __syncthreads();
     forward17<T, false, false, false>(r, dx0, false);   // DX of the starting point
+    const bool sbox = a.sbox != 0;
+    const bool xlane = sbox && j < NX17;
+    if (valid && xlane) {   // state rows: s = max(distance to the bound, theta w), lambda = 1
+      for (int k = 1; k < N; ++k) {
+        const T xb = r.w.XB[(int64_t)k * NX17 + j], y = r.w.DX[(int64_t)k * NX17 + j];
+        const T lb = W.lbx[j] - xb, ub = W.ubx[j] - xb, tw = T(IPM17_THETA) * (ub - lb);
+        T* ix = r.w.IX + (int64_t)k * 4 * NX17 + j;
+        ix[0] = fmax(y - lb, tw);
+        ix[NX17] = fmax(ub - y, tw);
+        ix[2 * NX17] = T(1);
+        ix[3 * NX17] = T(1);
+      }
+    }
     __syncthreads();
+    const T rows = T(N * NU17 + (sbox ? (N - 1) * NX17 : 0));
     bool done = false;
+    T prev_alpha = T(1);
     for (int it = 0; it < a.max_as_iter; ++it) {
       // duality measure mu = mean(lambda s) (input lanes sum over stages, then over components)
       T part = T(0);
@@ -477,14 +530,32 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
           part += ip[6 + ju] * (ip[ju] - (lbm - ubk)) + ip[12 + ju] * ((ubm - ubk) - ip[ju]);
         }
       }
+      T res = T(0);
+      if (xlane) {
+        for (int k = 1; k < N; ++k) {
+          const SRow17<T> sr(r, k);
+          part += sr.ll * sr.sl + sr.lu * sr.su;
+          res = fmax(res, fmax(fabs(sr.rl), fabs(sr.ru)));
+        }
+      }
       T mu = T(0);
 #pragma unroll
-      for (int m = 0; m < NU17; ++m) mu += __shfl(part, q * L17 + NX17 + m);
-      mu /= T(2 * N * NU17);
-      done = done || !(mu > T(IPM17_TOL));
+      for (int m = 0; m < NZ17; ++m) mu += __shfl(part, q * L17 + m);
+      mu /= T(2) * rows;
+      if (sbox) {
+#pragma unroll
+        for (int m = 0; m < NX17; ++m) res = fmax(res, __shfl(res, q * L17 + m));
+      }
+      done = done || (!(mu > T(IPM17_TOL)) && !(res > T(1e-9)));
       if (__all(done || !valid)) break;
-      const T smu = T(IPM17_SIGMA) * mu;
-      if (!riccati17_backward<T, true>(r, smu)) st = MPCB_STATUS_QP_FAIL;
+      // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
+      const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
+      if (!riccati17_backward<T, true>(r, smu) && !done) {
+        // a Newton system that lost positive definiteness near the solution (lambda / s ~ 1e18 on
+        // an active row): keep the current iterate as converged; earlier it is a failure
+        if (!(mu > T(IPM17_BREAK)) && !(res > T(1e-9))) done = true;
+        else st = MPCB_STATUS_QP_FAIL;
+      }
       __syncthreads();
       forward17<T, true, true, false>(r, T(0), false);   // the Newton step -> DDX, DDU
       __syncthreads();
@@ -504,10 +575,30 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
           if (dlu < T(0)) amax = fmin(amax, -lu / dlu);
         }
       }
+      if (xlane) {
+        for (int k = 1; k < N; ++k) {
+          const SRow17<T> sr(r, k);
+          const T dy = r.w.DDX[(int64_t)k * NX17 + j];
+          const T dsl = dy + sr.rl, dsu = sr.ru - dy;
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          if (dsl < T(0)) amax = fmin(amax, -sr.sl / dsl);
+          if (dsu < T(0)) amax = fmin(amax, -sr.su / dsu);
+          if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
+          if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
+        }
+      }
 #pragma unroll
-      for (int m = 0; m < NU17; ++m) amax = fmin(amax, __shfl(amax, q * L17 + NX17 + m));
-      const T alpha = done ? T(0) : fmin(T(1), T(IPM17_TAU) * amax);
-      if (valid && ilane) {
+      for (int m = 0; m < NZ17; ++m) amax = fmin(amax, __shfl(amax, q * L17 + m));
+      // (a finished instance skips the updates: its Newton step may be non-finite)
+      const T alpha = fmin(T(1), T(IPM17_TAU) * amax);
+      prev_alpha = alpha;
+      if (!done && alpha < T(IPM17_STALL)) {
+        // collapsed step: converged near the solution (conditioning limit), else an infeasible QP
+        if (mu > T(IPM17_BREAK) || res > T(1e-9)) st = MPCB_STATUS_QP_FAIL;
+        done = true;
+      }
+      if (!done && valid && ilane) {
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
           T* ip = r.w.IP + (int64_t)k * 18;
@@ -520,7 +611,21 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
           ip[12 + ju] = lu + alpha * dlu;
         }
       }
-      if (valid && j < NX17) {
+      if (!done && valid && xlane) {   // state-row slacks and multipliers (before DX moves: the residuals use it)
+        for (int k = 1; k < N; ++k) {
+          const SRow17<T> sr(r, k);
+          const T dy = r.w.DDX[(int64_t)k * NX17 + j];
+          const T dsl = dy + sr.rl, dsu = sr.ru - dy;
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          T* ix = r.w.IX + (int64_t)k * 4 * NX17 + j;
+          ix[0] = sr.sl + alpha * dsl;
+          ix[NX17] = sr.su + alpha * dsu;
+          ix[2 * NX17] = sr.ll + alpha * dll;
+          ix[3 * NX17] = sr.lu + alpha * dlu;
+        }
+      }
+      if (!done && valid && j < NX17) {
         for (int k = 0; k <= N; ++k) r.w.DX[(int64_t)k * NX17 + j] += alpha * r.w.DDX[(int64_t)k * NX17 + j];
       }
       __syncthreads();

@@ -32,7 +32,9 @@ def test_full_model_matches_reference_defaults():
         assert np.array_equal(getattr(cfg, a), getattr(ref, a)), a
     assert cfg.t_blast == pytest.approx(21.582, rel=1e-12)
     assert info['idxbx'] == list(range(17)) and len(info['lbx']) == 17
-    assert any('state box' in str(x.message) for x in w)
+    assert not any('state box' in str(x.message) for x in w)        # applied on the 17/6 model
+    assert np.array_equal(cfg.lbx, info['lbx']) and np.array_equal(cfg.ubx, info['ubx'])
+    assert cfg.lbx[2] == 0.0 and cfg.ubx[12] == pytest.approx(1.22173)
     assert np.array_equal(cfg.lbu, [0, 0, 0, 0, -0.0872665, -0.0872665])
     assert np.array_equal(cfg.ubu, [65, 65, 65, 65, 0.0872665, 0.0872665])
 
@@ -42,7 +44,7 @@ def test_slice_12_4_matches_baseline_config():
         warnings.simplefilter('ignore')
         cfg, _ = load_acados_ocp_json(_nested(), slice_12_4=True)
     base = MPCConfig(N=60)
-    assert (cfg.nx, cfg.nu) == (12, 4)
+    assert (cfg.nx, cfg.nu) == (12, 4) and cfg.lbx is None
     for a in ('Q', 'R', 'QN'):
         assert np.array_equal(getattr(cfg, a), getattr(base, a)), a
     assert np.array_equal(cfg.lbu, np.zeros(4)) and np.array_equal(cfg.ubu, np.full(4, 65.0))

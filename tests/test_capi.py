@@ -27,13 +27,13 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.EXPORTS) == set(declared)
-    assert lib.mpcb_abi_version() == 2
+    assert lib.mpcb_abi_version() == 3
 
 
 def test_config_struct_layout_matches_header():
     from mpc_blaster_amd import _lib
-    # 8 int32 (32 B) + 8 doubles + J[9] + Q[289] + R[36] + QN[289] + lbu[6] + ubu[6]
-    n_doubles = 8 + 9 + 289 + 36 + 289 + 6 + 6
+    # 8 int32 (32 B) + 8 doubles + J[9] + Q[289] + R[36] + QN[289] + lbu[6] + ubu[6] + lbx[17] + ubx[17]
+    n_doubles = 8 + 9 + 289 + 36 + 289 + 6 + 6 + 17 + 17
     assert ctypes.sizeof(_lib.MpcbConfig) == 32 + 8 * n_doubles
     # compile a tiny C program against the header and compare sizeof/offsetof
     import subprocess
@@ -42,8 +42,9 @@ def test_config_struct_layout_matches_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "mpcb.h"
-int main(void) { printf("%zu %zu %zu %zu\n", sizeof(mpcb_config), offsetof(mpcb_config, dt),
-  offsetof(mpcb_config, Q), offsetof(mpcb_config, lbu)); return 0; }
+int main(void) { printf("%zu %zu %zu %zu %zu %zu\n", sizeof(mpcb_config), offsetof(mpcb_config, dt),
+  offsetof(mpcb_config, Q), offsetof(mpcb_config, lbu), offsetof(mpcb_config, box_x),
+  offsetof(mpcb_config, lbx)); return 0; }
 '''
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, 'm.c')
@@ -52,7 +53,8 @@ int main(void) { printf("%zu %zu %zu %zu\n", sizeof(mpcb_config), offsetof(mpcb_
         subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), c, '-o', exe])
         out = subprocess.check_output([exe]).decode().split()
     C = _lib.MpcbConfig
-    assert [int(v) for v in out] == [ctypes.sizeof(C), C.dt.offset, C.Q.offset, C.lbu.offset]
+    assert [int(v) for v in out] == [ctypes.sizeof(C), C.dt.offset, C.Q.offset, C.lbu.offset, C.box_x.offset,
+                                     C.lbx.offset]
 
 
 def test_create_without_gpu_fails_cleanly():

@@ -5,6 +5,8 @@ Tolerance: fp64 per-instance ||y_dev - y_oracle||_inf / max(||y_oracle||_inf, 1)
 X and U (north_star asks 1e-5); [A|B] and the plant step <= 1e-11 absolute.  fp32 is checked on
 u0 against the fp64 oracle with a 5e-4 normwise bound (achieved 2.7e-5; the alpha-rate weight 1e-5 of the
 reference makes the 6x6 input block ill-conditioned in single precision)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -16,6 +18,10 @@ pytestmark = pytest.mark.gpu
 
 LBU17 = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])   # JSON idxbu/lbu/ubu
 UBU17 = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+SB_LO = np.array([-1.5, -1.5, 0, -0.174532925, -0.174532925, -0.349066, -1.0, -1.0, -1.0, -0.0872665, -0.0872665,
+                  -0.0872665, -0.174532925, -0.523599, -1.5, -1.5, -2.5])     # statesBound (JSON lbx/ubx)
+SB_HI = np.array([1.5, 1.5, 5.0, 0.174532925, 0.174532925, 0.349066, 1.0, 1.0, 1.0, 0.0872665, 0.0872665,
+                  0.0872665, 1.22173, 0.523599, 1.5, 1.5, 2.5])
 
 
 def relerr(a, b):
@@ -121,7 +127,8 @@ def test_solve17_fp32_close_to_fp64_oracle():
     assert e <= 5e-4
 
 
-def test_acados_facade_full_model_runs_reference_loop():
+@pytest.mark.parametrize('states_bound', [False, True])
+def test_acados_facade_full_model_runs_reference_loop(states_bound):
     """simulation_blaster.py:56-107 through the compat facade on the FULL 17/6 model
     (blasterModel(..., full_model=True), the reference's controlBound enforced): set(0,'lbx'/'ubx'),
     set(k,'p'), cost_set(k,'yref'), solve(), get(0,'u'), then the plant integrator — against the
@@ -135,7 +142,8 @@ def test_acados_facade_full_model_runs_reference_loop():
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
         b = blasterModel(9.0, J, 0.3434, 0.3475, N, N / 30.0, 0.03, Q, R, 10 * Q, 2.2,
-                         np.full((2, 17), np.nan), np.stack([LBU17, UBU17]), full_model=True)
+                         np.stack([SB_LO, SB_HI]) if states_bound else np.full((2, 17), np.nan),
+                         np.stack([LBU17, UBU17]), full_model=True)
         b.generateModel()
         integrator, ocp_solver = b.generateController()
     rng = np.random.default_rng(4)
@@ -146,6 +154,9 @@ def test_acados_facade_full_model_runs_reference_loop():
     yref = np.zeros(23)
     yref[2], yref[14] = 3.5, 0.2                      # simulation_blaster.py:48
     spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17)          # controlBound (simulation_blaster.py:30)
+    if states_bound:                                    # statesBound (simulation_blaster.py:28-29)
+        spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17, lbx=SB_LO, ubx=SB_HI)
+    tol = 1e-7 if states_bound else 1e-9
     xbar, ubar = np.zeros((1, N + 1, 17)), np.zeros((1, N, 6))
     xr = np.broadcast_to(yref[:17], (1, N + 1, 17))
     ur = np.zeros((1, N, 6))
@@ -161,8 +172,9 @@ def test_acados_facade_full_model_runs_reference_loop():
         u = ocp_solver.get(0, 'u')
         o = mpc_solve17(x[None], xr, ur, spec, p[None], mode='iterate', xbar=xbar, ubar=ubar)
         xbar, ubar = o['X'], o['U']
-        assert relerr(u[None], o['u0']).max() < 1e-9
-        assert relerr(ocp_solver.get(N, 'x')[None], o['X'][:, N]).max() < 1e-9
+        assert o['status'][0] == 0
+        assert relerr(u[None], o['u0']).max() < tol
+        assert relerr(ocp_solver.get(N, 'x')[None], o['X'][:, N]).max() < tol
         integrator.set('x', x)
         integrator.set('u', u)
         assert integrator.solve() == 0
@@ -210,3 +222,58 @@ def test_solve17_input_box_matches_oracle_interior_point(mode):
           f'{act.mean():.1%} of (k, m) at a bound, oracle iterations max {o["iters"].max()}')
     assert max(e) <= 1e-9
     assert eb <= 1e-5
+
+
+def _sbox_inputs(B, N, seed):
+    """x0 inside a quarter of the reference's state box (tests/golden/ocp_json_pin.json)."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'ocp_json_pin.json')))
+    lbx, ubx = np.array(d['lbx']), np.array(d['ubx'])
+    x0, xref, uref, p = _inputs(B, N, seed)
+    rng = np.random.default_rng(seed + 1)
+    x0 = rng.uniform(0.25 * lbx, 0.25 * ubx, (B, 17))
+    x0[:, 2] = 3.5 + rng.uniform(-0.5, 0.5, B)
+    return x0, xref, uref, p, lbx, ubx
+
+
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_solve17_state_box_matches_oracle_interior_point(mode):
+    """The reference's state box (JSON idxbx, stages 1..N-1) with its input box: the device
+    interior point equals the oracle's iteration (<= 1e-6: both stop at the conditioning limit
+    near the solution, mu ~ 1e-12 with lambda / s ~ 1e16 on active rows, where the iterate is
+    determined to ~1e-7 and one more or fewer step shows) and carries a KKT certificate of the
+    condensed QP (oracle.ocp.dense_kkt_certificate: NNLS multipliers >= 0, stationarity,
+    feasibility, and a duality gap that bounds the suboptimality)."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    from oracle.ocp import dense_kkt_certificate
+    N, B = 20, 24
+    x0, xref, uref, p, lbx, ubx = _sbox_inputs(B, N, 41)
+    m = BatchedMPC(MPCConfig.full(N=N, lbu=LBU17, ubu=UBU17, lbx=lbx, ubx=ubx), max_batch=B)
+    m.set_params(p)
+    spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17, lbx=lbx, ubx=ubx)
+    kw = {}
+    if mode == 'iterate':
+        rng = np.random.default_rng(42)
+        kw = dict(xbar=x0[:, None, :] + rng.normal(0, 0.01, (B, N + 1, 17)),
+                  ubar=uref + rng.normal(0, 0.5, (B, N, 6)))
+        m.solve_iterate(x0, kw['xbar'], kw['ubar'], xref, uref)
+    else:
+        m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, spec, p, mode=mode, **kw)
+    assert (o['status'] == 0).all()
+    assert (m.get_status().cpu().numpy() == 0).all()
+    X = m.get_state_trajectory().cpu().numpy()
+    U = m.get_input_trajectory().cpu().numpy()
+    assert (X[:, 1:N] >= lbx - 1e-9).all() and (X[:, 1:N] <= ubx + 1e-9).all()
+    n_act = ((o['X'][:, 1:N] - lbx < 1e-6) | (ubx - o['X'][:, 1:N] < 1e-6)).sum()
+    assert n_act >= B * 5                              # the state box is active
+    e = [relerr(m.get_control().cpu().numpy(), o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max()]
+    stat, viol, gap = dense_kkt_certificate(o['A'], o['B'], o['gap'], x0 - o['xbar'][:, 0], o['xbar'], o['ubar'],
+                                            np.broadcast_to(xref, (B, N + 1, 17)),
+                                            np.broadcast_to(uref, (B, N, 6)), spec, U - o['ubar'], lbx=lbx, ubx=ubx)
+    print(f'17/6 state box fp64 {mode}: u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e} vs oracle; KKT certificate: '
+          f'stationarity {stat.max():.1e} violation {viol.max():.1e} duality gap {gap.max():.1e}; '
+          f'{n_act} active state rows, oracle iterations max {o["iters"].max()}')
+    assert max(e) <= 1e-6
+    assert stat.max() <= 1e-8 and viol.max() <= 1e-9 and gap.max() <= 1e-5

@@ -62,7 +62,7 @@ def test_library_is_the_native_hip_build():
     from mpc_blaster_amd import _lib
     lib = _lib.load()
     assert os.path.basename(lib._name) == 'libmpcblaster.so'
-    assert lib.mpcb_abi_version() == 2
+    assert lib.mpcb_abi_version() == 3
 
 
 def test_linearize_matches_oracle_fp64():

@@ -25,6 +25,8 @@ def main():
     ap.add_argument('--dtype', default='f64')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--bounds', default='none', choices=['none', 'input', 'all'],
+                    help="the reference's controlBound (input) and statesBound (all) by the interior point")
     args = ap.parse_args()
     import torch
     from mpc_blaster_amd import BatchedMPC, MPCConfig
@@ -43,7 +45,19 @@ def main():
     p = np.zeros((B, 25))
     p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
     p[:, 24] = 2.2 * 9.81
-    cfg = MPCConfig.full(N=N, dtype=args.dtype)
+    lbu = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])     # simulation_blaster.py:28-30
+    ubu = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+    lbx = np.array([-1.5, -1.5, 0, -0.174532925, -0.174532925, -0.349066, -1.0, -1.0, -1.0, -0.0872665,
+                    -0.0872665, -0.0872665, -0.174532925, -0.523599, -1.5, -1.5, -2.5])
+    kw = {}
+    if args.bounds != 'none':
+        kw.update(lbu=lbu, ubu=ubu)
+    if args.bounds == 'all':
+        kw.update(lbx=lbx, ubx=-lbx)
+        kw['ubx'][[2, 12]] = 5.0, 1.22173
+        x0 = np.clip(x0, 0.5 * lbx, 0.5 * kw['ubx'])
+        x0[:, 2] = 3.5 + rng.uniform(-0.5, 0.5, B)
+    cfg = MPCConfig.full(N=N, dtype=args.dtype, **kw)
     m = BatchedMPC(cfg, max_batch=B)
     dt = cfg.torch_dtype
     dev = 'cuda:0'
@@ -62,7 +76,7 @@ def main():
     bad = int((outs[3] != 0).sum().item())
     print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
                       'unit': 'solves/s', 'ms_per_step': el / args.steps * 1e3, 'batch': B,
-                      'dtype': args.dtype, 'bad_status': bad,
+                      'dtype': args.dtype, 'bad_status': bad, 'bounds': args.bounds,
                       'config': 'reference OCP (acados_ocp_blasterModel.json), random x0 + POC params'}))
 
 
