@@ -29,6 +29,14 @@ namespace mpcb {
 #ifndef MPCB_BOX_WAVES
 #define MPCB_BOX_WAVES 2
 #endif
+// 1: a masked pass restarts at the highest changed stage from a stored value-function snapshot
+// (P_k, p_k written by every pass); 0: every masked pass runs the full recursion, no snapshots
+#ifndef MPCB_BOX_RESTART
+#define MPCB_BOX_RESTART 1
+#endif
+#ifndef MPCB_BOX_FWD_DEPTH   // forward-pass prefetch depth (stages) in the active-set kernel
+#define MPCB_BOX_FWD_DEPTH 1
+#endif
 
 // MODE (the same passes serve three uses):
 //   PASS_BOX   input boxes: active-set iterations (the first backward pass is P2's)
@@ -290,7 +298,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? L.P[jx * NX + i] : T(0);
-        if (BOX && act && valid && j < NX && k > 0) {   // snapshot P_k, p_k for a later restart
+        if (MPCB_BOX_RESTART && BOX && act && valid && j < NX && k > 0) {   // snapshot P_k, p_k for a later restart
           T* ps = soa(a.PS, k, PS_REC, nb, c) + j * SS;
 #pragma unroll
           for (int i = 0; i < NX; ++i) ps[i * NX * SS] = Pc[i];
@@ -308,7 +316,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     // prefetched DEPTH stages ahead (two register sets, slots fixed by unrolling by two; one
     // stage in the register-heavy active-set kernel): own ybar component; input lanes: row ju of
     // the gains (K | k) and of the stage Hessian (+ h_u); state lanes: row jx of [A|B], the gap
-    constexpr int DEPTH = BOX ? 1 : 2;
+    constexpr int DEPTH = BOX ? MPCB_BOX_FWD_DEPTH : 2;
     T fyb[2], fa[2][NZ + 1], fb[2][NX + 1];
     auto fload = [&](int k, auto sl_tag) {
       constexpr int sl = decltype(sl_tag)::value;
@@ -432,7 +440,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       }
     }
     // (the first masked pass is complete: P2 stored no snapshots)
-    kc = changed ? (it == 0 ? N - 1 : 63 - __clzll(changed)) : -1;
+    kc = changed ? ((it == 0 || !MPCB_BOX_RESTART) ? N - 1 : 63 - __clzll(changed)) : -1;
     if (!done && gconv) done = true;
     if (__all(done || !valid)) break;
     if (it + 1 >= a.max_as_iter) {

@@ -239,8 +239,12 @@ struct SRow17 {
   }
 };
 
-template <class T, bool IPM>
+// The IPM switch is the launch's box flag read at run time, on purpose: the compile-time
+// specialisation of the unconstrained pass scheduled the stage loop into 527 spilled VGPRs
+// (1976 B scratch per lane in fp64); with the flag opaque to the compiler it spills nothing.
+template <class T>
 __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
+  const bool IPM = r.a.box != 0;
   FullLds<T>& L = r.L;
   const int j = r.j, jd = r.jd, jx = r.jx, ju = r.ju, N = r.N;
   const Weights17<T>& W = *r.a.W;
@@ -272,7 +276,7 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
     if (j < NX17) L.gp[j] = IPM ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
     {
       T yb = (j < NX17) ? r.w.XB[(int64_t)k * NX17 + jx] : r.w.UB[(int64_t)k * NU17 + ju];
-      if constexpr (IPM) yb += (j < NX17) ? r.w.DX[(int64_t)k * NX17 + jx] : r.w.IP[(int64_t)k * 18 + ju];
+      if (IPM) yb += (j < NX17) ? r.w.DX[(int64_t)k * NX17 + jx] : r.w.IP[(int64_t)k * 18 + ju];
       const T yr = (j < NX17) ? r.xr[(int64_t)k * NX17 + jx] : r.ur[(int64_t)k * NU17 + ju];
       L.v[j] = r.dir ? yb - yr : T(0);
     }
@@ -308,7 +312,7 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
       hj += wgt * L.v[i];
       if (i % 2 == 1) wave_lds_sync();
     }
-    if constexpr (IPM) {   // state-box rows of this stage: barrier terms on the state lane's diagonal
+    if (IPM) {   // state-box rows of this stage: barrier terms on the state lane's diagonal
       if (r.a.sbox && j < NX17 && k > 0) {
         const SRow17<T> sr(r, k);
         const T Dj = sr.ll / sr.sl + sr.lu / sr.su;
@@ -329,7 +333,7 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
       for (int n = 0; n < NU17; ++n) Huu[m * NU17 + n] = L.Hu[(NX17 + n) * NU17 + m];
       ht[m] = L.hv[NX17 + m];
     }
-    if constexpr (IPM) {   // barrier terms of this stage (instance-uniform values)
+    if (IPM) {   // barrier terms of this stage (instance-uniform values)
       const T* ip = r.w.IP + (int64_t)k * 18;
 #pragma unroll
       for (int m = 0; m < NU17; ++m) {
@@ -485,7 +489,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
   int32_t st = MPCB_STATUS_OK;
   bool fin;
   if constexpr (!BOX) {
-    if (!riccati17_backward<T, false>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
+    if (!riccati17_backward<T>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
     __syncthreads();   // K and k are read back across lanes
     fin = forward17<T, true, false, true>(r, dx0, valid);
   } else {
@@ -550,7 +554,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       if (__all(done || !valid)) break;
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
       const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
-      if (!riccati17_backward<T, true>(r, smu) && !done) {
+      if (!riccati17_backward<T>(r, smu) && !done) {
         // a Newton system that lost positive definiteness near the solution (lambda / s ~ 1e18 on
         // an active row): keep the current iterate as converged; earlier it is a failure
         if (!(mu > T(IPM17_BREAK)) && !(res > T(1e-9))) done = true;

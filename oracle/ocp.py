@@ -543,3 +543,30 @@ def dense_kkt_certificate(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, du, lbx
         viol[b] = max(0.0, v.max())
         dgap[b] = float(lam @ -v[act]) if len(act) else 0.0
     return stat, viol, dgap
+
+
+def lp_box_feasible(A, Bm, gap, dx0, xbar, ubar, spec, lbx, ubx):
+    """Independent check (tests only): is the box QP of each instance feasible?  The condensed
+    rows (input box; state box on stages 1..N-1) as an LP feasibility problem for SciPy's HiGHS.
+    Returns a bool per instance."""
+    from scipy.optimize import linprog
+
+    Bsz, N = xbar.shape[0], spec.N
+    NX, NU = A.shape[-1], Bm.shape[-1]
+    out = np.zeros(Bsz, dtype=bool)
+    for b in range(Bsz):
+        c = np.zeros((N + 1, NX))
+        G = np.zeros((N + 1, NX, N * NU))
+        c[0] = dx0[b]
+        for k in range(N):
+            c[k + 1] = A[b, k] @ c[k] + gap[b, k]
+            G[k + 1] = A[b, k] @ G[k]
+            G[k + 1][:, k * NU:(k + 1) * NU] += Bm[b, k]
+        Gx = G[1:N].reshape(-1, N * NU)
+        lo = (np.asarray(lbx) - xbar[b, 1:N] - c[1:N]).ravel()
+        hi = (np.asarray(ubx) - xbar[b, 1:N] - c[1:N]).ravel()
+        bnds = list(zip((np.asarray(spec.lbu) - ubar[b]).ravel(), (np.asarray(spec.ubu) - ubar[b]).ravel()))
+        r = linprog(np.zeros(N * NU), A_ub=np.vstack([Gx, -Gx]), b_ub=np.concatenate([hi, -lo]), bounds=bnds,
+                    method='highs')
+        out[b] = r.status == 0
+    return out

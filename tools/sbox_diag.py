@@ -30,7 +30,7 @@ def condense(A, Bm, gap, dx0, N):
     return Phi, c
 
 
-def feasible(A, Bm, gap, dx0, xbar, ubar, N):
+def feasible(A, Bm, gap, dx0, xbar, ubar, N):   # see also oracle.ocp.lp_box_feasible
     Phi, c = condense(A, Bm, gap, dx0, N)
     NU = Bm.shape[-1]
     G = Phi[1:N].reshape(-1, N * NU)
