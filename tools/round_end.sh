@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-end validation on the GPU box: full GPU suite, smoke, default bench, the bench through
+# torch.distributed.run (1 rank: the multi-GPU code path), profiles (tools/collect_profiles.sh)
+# and the 17/6 benches with a kernel-stats profile.  Output: gpurun_out/$1
+set -e
+O=gpurun_out/${1:-round_end}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_torchrun.log 2>&1
+bash tools/collect_profiles.sh ${1:-round_end}
+for b in none input all; do
+  timeout -k 10 200 python tools/bench_full17.py --bounds $b --steps 5 > $O/bench_full17_$b.log 2>&1
+done
+timeout -k 10 200 python tools/bench_full17.py --dtype f32 --batch 16384 --steps 5 > $O/bench_full17_f32.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_full17 -o run -- \
+  python3 tools/bench_full17.py --steps 5 > $O/stats_full17.log 2>&1
+echo round_end_done
