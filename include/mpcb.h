@@ -88,7 +88,9 @@ int mpcb_path(const mpcb_handle* h);
 /* Optional device timing of later solves: HIP events recorded on the launch stream around each
  * kernel phase.  ``mpcb_last_timing`` waits for the last timed solve and writes the device
  * milliseconds of its phases: ms[0] nominal rollout, ms[1] Riccati (the dominant kernel; the
- * single launch on the fused / box paths), ms[2] forward pass.  Summed over chunks (up to 64).
+ * single launch on the fused / box paths), ms[2] forward pass; on the 17/6 model ms[0] nominal17,
+ * ms[1] riccati17 (Riccati + forward, the interior point with boxes), ms[2] lin17ws (the
+ * stage-parallel linearisation).  Summed over chunks (up to 64).
  * No reference counterpart (acados' ``get_stats('time_tot')`` is host wall time). */
 int mpcb_set_timing(mpcb_handle* h, int enable);
 int mpcb_last_timing(mpcb_handle* h, float ms[3]);

@@ -69,9 +69,12 @@ class BatchedMPC:
         _lib.check(self.lib.mpcb_set_timing(self._h, 1 if enable else 0))
 
     def last_timing(self) -> dict:
-        """Device ms of the last timed solve's phases: nominal, riccati (dominant), forward."""
+        """Device ms of the last timed solve's phases: nominal, riccati (dominant), forward
+        (17/6 model: nominal, riccati = Riccati + forward or the interior point, linearise)."""
         ms = (ctypes.c_float * 3)()
         _lib.check(self.lib.mpcb_last_timing(self._h, ms))
+        if self.nx == 17:
+            return dict(nominal=ms[0], riccati=ms[1], linearise=ms[2])
         return dict(nominal=ms[0], riccati=ms[1], forward=ms[2])
 
     def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):

@@ -309,13 +309,17 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.box = h->cfg.box_u;
     a.sbox = h->cfg.box_x;
     a.max_as_iter = h->cfg.max_as_iter;
+    int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       a.b0 = b0;
       a.nb = (B - b0 < h->chunk) ? B - b0 : h->chunk;
-      hipError_t e = launch_full17<T>(a, (hipStream_t)stream);
+      hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
+      hipError_t e = launch_full17<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "full17 launch: %s", hipGetErrorString(e));
+      ++chunk_i;
     }
-    h->timed_chunks = 0;   // per-phase timing is implemented for the 12/4 kernels
+    h->timed_chunks = h->timing ? (chunk_i < mpcb_handle::TCHUNKS ? chunk_i : mpcb_handle::TCHUNKS) : 0;
+    h->timed_split = 1;
     return MPCB_OK;
   }
   if (h->split) {
@@ -421,7 +425,9 @@ extern "C" int mpcb_last_timing(mpcb_handle* h, float* ms) {
       hipError_t e = hipEventSynchronize(h->ev[c][p + 1]);
       if (e == hipSuccess) e = hipEventElapsedTime(&t, h->ev[c][p], h->ev[c][p + 1]);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "event timing: %s", hipGetErrorString(e));
-      ms[h->timed_split ? p : 1] += t;
+      // 17/6: the phases run nominal17, lin17ws, riccati17 (+ forward); ms[1] stays the Riccati
+      const int slot = !h->timed_split ? 1 : (h->full ? (p == 0 ? 0 : (p == 1 ? 2 : 1)) : p);
+      ms[slot] += t;
     }
   }
   return MPCB_OK;

@@ -221,7 +221,8 @@ __host__ __device__ constexpr int64_t full17_elems(int N) {
          2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17) + 4 * (int64_t)(N + 1) * NX17;
 }
 
-template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st);
+// ev (nullable): 4 events recorded before nominal17, after it, after lin17ws and after riccati17.
+template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev = nullptr);
 template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
                               const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st);

@@ -687,13 +687,17 @@ __global__ void __launch_bounds__(64) sim17_kernel(int64_t B, T h, Model<T> M, c
   for (int i = 0; i < NX17; ++i) xo[b * NX17 + i] = xn[i];
 }
 
-template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st) {
+template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
+  if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + G17 - 1) / G17)), dim3(64), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[2], st);
   if (a.box)
     hipLaunchKernelGGL((riccati17_kernel<T, true>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL((riccati17_kernel<T, false>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[3], st);
   return hipGetLastError();
 }
 template <class T>
@@ -712,8 +716,8 @@ hipError_t launch_sim_step17(int64_t B, T h, const Model<T>& M, const T* p, int6
   return hipGetLastError();
 }
 
-template hipError_t launch_full17<double>(const FullArgs<double>&, hipStream_t);
-template hipError_t launch_full17<float>(const FullArgs<float>&, hipStream_t);
+template hipError_t launch_full17<double>(const FullArgs<double>&, hipStream_t, hipEvent_t*);
+template hipError_t launch_full17<float>(const FullArgs<float>&, hipStream_t, hipEvent_t*);
 template hipError_t launch_linearize17<double>(int64_t, int, double, const Model<double>&, const double*,
                                                int64_t, const double*, const double*, double*, double*,
                                                double*, hipStream_t);

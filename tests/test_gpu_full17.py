@@ -315,3 +315,19 @@ def test_solve17_state_box_infeasible_instances_flagged():
                                             lbx=lbx, ubx=ubx)
     # (gap bounds f(z) - f*; the objectives are ~1e3 here, so 1e-4 is 1e-7 relative)
     assert stat.max() <= 1e-8 and viol.max() <= 1e-9 and gap.max() <= 1e-4, (stat.max(), viol.max(), gap.max())
+
+
+def test_full17_phase_timing_events():
+    """mpcb_set_timing / mpcb_last_timing on the 17/6 path: nominal17, riccati17, lin17ws device
+    ms from HIP events, and timing changes no result."""
+    N, B = 12, 16
+    m = _mpc(N, max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 5)
+    m.set_params(p)
+    a = m.solve(x0, xref, uref).clone()
+    m.set_timing(True)
+    b = m.solve(x0, xref, uref)
+    t = m.last_timing()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert t['nominal'] > 0 and t['riccati'] > 0 and t['linearise'] > 0

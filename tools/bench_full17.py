@@ -74,9 +74,27 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     bad = int((outs[3] != 0).sum().item())
+    m.set_timing(True)                     # one more solve with per-phase HIP events
+    m.solve(x0t, xrt, urt, out=outs)
+    ph = m.last_timing()
+    m.set_timing(False)
+    # riccati17 algorithmic flops per stage (dense counts, nx = 17, nu = 6, nz = 23): P[A|B]
+    # 2 nx^2 nz, [A|B]' P [A|B] 2 nz^2 nx, Cholesky nu^3/3 + K, k solves 2 nu^2 (nx + 1),
+    # P update 2 nx^2 nu, vector terms 2 nx^2 + 2 nz nx + 2 (nx^2 + nu^2) + 2 nx nu, and the
+    # forward pass 2 nu nx + 2 nx nz
+    nx_, nu_, nz_ = 17, 6, 23
+    fl = (2 * nx_ * nx_ * nz_ + 2 * nz_ * nz_ * nx_ + nu_ ** 3 / 3 + 2 * nu_ * nu_ * (nx_ + 1) + 2 * nx_ * nx_ * nu_
+          + 2 * nx_ * nx_ + 2 * nz_ * nx_ + 2 * (nx_ * nx_ + nu_ * nu_) + 2 * nx_ * nu_ + 2 * nu_ * nx_ + 2 * nx_ * nz_)
+    peak = 78.6 if args.dtype == 'f64' else 157.3
+    roof = None
+    if args.bounds == 'none':
+        ach = fl * N * B / (ph['riccati'] * 1e-3) / 1e12
+        roof = {'bound': 'mfma', 'kernel': 'riccati17_kernel', 'flop_per_stage': fl, 'achieved': ach,
+                'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak}
     print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
                       'unit': 'solves/s', 'ms_per_step': el / args.steps * 1e3, 'batch': B,
                       'dtype': args.dtype, 'bad_status': bad, 'bounds': args.bounds,
+                      'phase_ms': ph, 'roofline': roof,
                       'config': 'reference OCP (acados_ocp_blasterModel.json), random x0 + POC params'}))
 
 
