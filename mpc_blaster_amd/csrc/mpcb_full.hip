@@ -268,18 +268,28 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
     wave_lds_sync();
   }
   bool qp_ok = true;
-  for (int k = N - 1; k >= 0; --k) {
-    T col[NX17];
+  // stage data one stage ahead (column jd of [A|B], the gap, the own y - yref component): the
+  // loads of stage k - 1 are in flight while stage k computes (without it 59 % of the wave time
+  // sat in s_waitcnt: PMC)
+  T ncol[NX17], ngp, ne;
+  auto prefetch = [&](int k) {
     const T* ABk = r.w.AB + ((int64_t)k * NZ17 + jd) * NX17;
 #pragma unroll
-    for (int i = 0; i < NX17; ++i) col[i] = ABk[i];
-    if (j < NX17) L.gp[j] = IPM ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
-    {
-      T yb = (j < NX17) ? r.w.XB[(int64_t)k * NX17 + jx] : r.w.UB[(int64_t)k * NU17 + ju];
-      if (IPM) yb += (j < NX17) ? r.w.DX[(int64_t)k * NX17 + jx] : r.w.IP[(int64_t)k * 18 + ju];
-      const T yr = (j < NX17) ? r.xr[(int64_t)k * NX17 + jx] : r.ur[(int64_t)k * NU17 + ju];
-      L.v[j] = r.dir ? yb - yr : T(0);
-    }
+    for (int i = 0; i < NX17; ++i) ncol[i] = ABk[i];
+    ngp = (j < NX17 && !IPM) ? r.w.GP[(int64_t)k * NX17 + jx] : T(0);
+    T yb = (j < NX17) ? r.w.XB[(int64_t)k * NX17 + jx] : r.w.UB[(int64_t)k * NU17 + ju];
+    if (IPM) yb += (j < NX17) ? r.w.DX[(int64_t)k * NX17 + jx] : r.w.IP[(int64_t)k * 18 + ju];
+    const T yr = (j < NX17) ? r.xr[(int64_t)k * NX17 + jx] : r.ur[(int64_t)k * NU17 + ju];
+    ne = r.dir ? yb - yr : T(0);
+  };
+  prefetch(N - 1);
+  for (int k = N - 1; k >= 0; --k) {
+    T col[NX17];
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) col[i] = ncol[i];
+    if (j < NX17) L.gp[j] = ngp;
+    L.v[j] = ne;
+    if (k > 0) prefetch(k - 1);
 #pragma unroll
     for (int i = 0; i < NX17; ++i) L.X[j * NX17 + i] = col[i];
     wave_lds_sync();
