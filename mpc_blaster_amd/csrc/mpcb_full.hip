@@ -409,19 +409,43 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
   const bool ilane = j >= NX17 && r.dir;
   const int64_t b = a.b0 + (r.w.XB - a.ws) / full17_elems(N);
   bool fin = true;
+  // the stage's row data one stage ahead: state lanes row j of [A_k | B_k] and the gap, input
+  // lanes row ju of (K_k | k_k) (or the iterate's du)
+  T nr[NZ17 + 1];
+  auto prefetch = [&](int k) {
+    if (j < NX17) {
+      const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
+#pragma unroll
+      for (int l = 0; l < NZ17; ++l) nr[l] = ABk[l * NX17 + j];
+      nr[NZ17] = STEP ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
+    } else if (ilane) {
+      if constexpr (GAIN) {
+        const T* Kk = r.w.KR + (int64_t)k * KR_N;
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) nr[i] = Kk[i * NU17 + ju];
+        nr[NX17] = Kk[NU17 * NX17 + ju];
+      } else {
+        nr[0] = r.w.IP[(int64_t)k * 18 + ju];
+      }
+    }
+  };
+  prefetch(0);
   for (int k = 0; k < N; ++k) {
+    T cr[NZ17 + 1];
+#pragma unroll
+    for (int i = 0; i <= NZ17; ++i) cr[i] = nr[i];
+    if (k + 1 < N) prefetch(k + 1);
     if (j < NX17) L.z[j] = dxj;
     wave_lds_sync();
     T duj = T(0);
     if (ilane) {
       if constexpr (GAIN) {
-        const T* Kk = r.w.KR + (int64_t)k * KR_N;
-        T acc = Kk[NU17 * NX17 + ju];
+        T acc = cr[NX17];
 #pragma unroll
-        for (int i = 0; i < NX17; ++i) acc += Kk[i * NU17 + ju] * L.z[i];
+        for (int i = 0; i < NX17; ++i) acc += cr[i] * L.z[i];
         duj = acc;
       } else {
-        duj = r.w.IP[(int64_t)k * 18 + ju];
+        duj = cr[0];
       }
       L.z[j] = duj;
     }
@@ -437,10 +461,9 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
       if (OUT && write && k == 0) a.u0[b * NU17 + ju] = uo;
     }
     if (j < NX17) {
-      const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
-      T acc = STEP ? T(0) : r.w.GP[(int64_t)k * NX17 + j];
+      T acc = cr[NZ17];
 #pragma unroll
-      for (int l = 0; l < NZ17; ++l) acc += ABk[l * NX17 + j] * L.z[l];
+      for (int l = 0; l < NZ17; ++l) acc += cr[l] * L.z[l];
       dxj = acc;
     }
     fin = fin && ((dxj - dxj) == T(0));
@@ -538,6 +561,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       // duality measure mu = mean(lambda s) (input lanes sum over stages, then over components)
       T part = T(0);
       if (ilane) {
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
           const T* ip = r.w.IP + (int64_t)k * 18;
@@ -546,6 +570,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       }
       T res = T(0);
       if (xlane) {
+#pragma unroll 4
         for (int k = 1; k < N; ++k) {
           const SRow17<T> sr(r, k);
           part += sr.ll * sr.sl + sr.lu * sr.su;
@@ -576,6 +601,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       T amax = T(1) / T(IPM17_TAU);
       if (ilane) {
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
           const T* ip = r.w.IP + (int64_t)k * 18;
@@ -590,6 +616,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
         }
       }
       if (xlane) {
+#pragma unroll 4
         for (int k = 1; k < N; ++k) {
           const SRow17<T> sr(r, k);
           const T dy = r.w.DDX[(int64_t)k * NX17 + j];
@@ -613,6 +640,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
         done = true;
       }
       if (!done && valid && ilane) {
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + ju];
           T* ip = r.w.IP + (int64_t)k * 18;
@@ -626,6 +654,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
         }
       }
       if (!done && valid && xlane) {   // state-row slacks and multipliers (before DX moves: the residuals use it)
+#pragma unroll 4
         for (int k = 1; k < N; ++k) {
           const SRow17<T> sr(r, k);
           const T dy = r.w.DDX[(int64_t)k * NX17 + j];
