@@ -205,6 +205,14 @@ __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
 // backward pass computes K_k, k_k (workspace KR) for the LQ problem around the nominal
 // trajectory shifted by (SHIFT: the current IPM iterate dx, du; else 0), with the gaps (IPM: 0)
 // and, for IPM, the barrier terms D_k (added to the diagonal of H_uu) and d_k (added to h_u).
+// compiler fences inside the two LDS product loops of the backward pass (every YS columns of
+// Y = P [A|B], every GS rows of G): they bound how many LDS reads the scheduler hoists
+#ifndef MPCB_R17_YS
+#define MPCB_R17_YS 4
+#endif
+#ifndef MPCB_R17_GS
+#define MPCB_R17_GS 2
+#endif
 template <class T>
 struct R17 {
   FullLds<T>& L;
@@ -309,7 +317,7 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
       const T cl = col[l];
 #pragma unroll
       for (int i = 0; i < NX17; ++i) y[i] += L.P[l * NX17 + i] * cl;
-      if (l % 4 == 3) wave_lds_sync();
+      if (l % MPCB_R17_YS == MPCB_R17_YS - 1) wave_lds_sync();
     }
     T G[NZ17];
 #pragma unroll
@@ -320,7 +328,7 @@ __device__ __forceinline__ bool riccati17_backward(const R17<T>& r, T smu) {
       const T wgt = r.SW[jd * NZ17 + i];
       G[i] = acc + wgt;
       hj += wgt * L.v[i];
-      if (i % 2 == 1) wave_lds_sync();
+      if (i % MPCB_R17_GS == MPCB_R17_GS - 1) wave_lds_sync();
     }
     if (IPM) {   // state-box rows of this stage: barrier terms on the state lane's diagonal
       if (r.a.sbox && j < NX17 && k > 0) {
