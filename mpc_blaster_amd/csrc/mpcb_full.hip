@@ -484,7 +484,11 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
 }
 
 constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
-constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6;
+constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
+// fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit
+// long before 1e-12), so the tolerances scale with the precision; the result is checked
+// against the fp64 oracle in tests/test_gpu_full17.py
+constexpr double IPM17_TOL_F32 = 1e-6, IPM17_BREAK_F32 = 1e-3, IPM17_RES_F32 = 1e-5;
 
 // BOX: the input box lbu <= u <= ubu of the reference OCP (blastermodel.py:259-264; thrust
 // [0, 65] N, swivel rate +-0.0873 rad/s) by a primal-dual interior point over the Riccati
@@ -565,6 +569,9 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     const T rows = T(N * NU17 + (sbox ? (N - 1) * NX17 : 0));
     bool done = false;
     T prev_alpha = T(1);
+    constexpr bool F64 = sizeof(T) == 8;
+    const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
+    const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
     for (int it = 0; it < a.max_as_iter; ++it) {
       // duality measure mu = mean(lambda s) (input lanes sum over stages, then over components)
       T part = T(0);
@@ -593,14 +600,14 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
 #pragma unroll
         for (int m = 0; m < NX17; ++m) res = fmax(res, __shfl(res, q * L17 + m));
       }
-      done = done || (!(mu > T(IPM17_TOL)) && !(res > T(1e-9)));
+      done = done || (!(mu > ipm_tol) && !(res > ipm_res));
       if (__all(done || !valid)) break;
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
       const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
       if (!riccati17_backward<T>(r, smu) && !done) {
         // a Newton system that lost positive definiteness near the solution (lambda / s ~ 1e18 on
         // an active row): keep the current iterate as converged; earlier it is a failure
-        if (!(mu > T(IPM17_BREAK)) && !(res > T(1e-9))) done = true;
+        if (!(mu > ipm_brk) && !(res > ipm_res)) done = true;
         else st = MPCB_STATUS_QP_FAIL;
       }
       __syncthreads();
@@ -608,6 +615,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
       __syncthreads();
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       T amax = T(1) / T(IPM17_TAU);
+      bool dfin = true;   // a finite direction from strictly positive slacks (fp32 can lose both)
       if (ilane) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
@@ -617,6 +625,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
           const T sl = ip[ju] - (lbm - ubk), su = (ubm - ubk) - ip[ju];
           const T ll = ip[6 + ju], lu = ip[12 + ju];
           const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          dfin = dfin && sl > T(0) && su > T(0) && (d - d) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
           if (d < T(0)) amax = fmin(amax, -sl / d);
           if (d > T(0)) amax = fmin(amax, su / d);
           if (dll < T(0)) amax = fmin(amax, -ll / dll);
@@ -631,20 +640,29 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
           const T dsl = dy + sr.rl, dsu = sr.ru - dy;
           const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
           const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          dfin = dfin && (dsl - dsl) == T(0) && (dsu - dsu) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
           if (dsl < T(0)) amax = fmin(amax, -sr.sl / dsl);
           if (dsu < T(0)) amax = fmin(amax, -sr.su / dsu);
           if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
           if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
         }
       }
+      int dbad = dfin ? 0 : 1;
 #pragma unroll
-      for (int m = 0; m < NZ17; ++m) amax = fmin(amax, __shfl(amax, q * L17 + m));
+      for (int m = 0; m < NZ17; ++m) {
+        amax = fmin(amax, __shfl(amax, q * L17 + m));
+        dbad |= __shfl(dbad, q * L17 + m);
+      }
       // (a finished instance skips the updates: its Newton step may be non-finite)
       const T alpha = fmin(T(1), T(IPM17_TAU) * amax);
       prev_alpha = alpha;
+      if (!done && dbad) {   // no usable direction: converged near the solution, else a failure
+        if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
+        done = true;
+      }
       if (!done && alpha < T(IPM17_STALL)) {
         // collapsed step: converged near the solution (conditioning limit), else an infeasible QP
-        if (mu > T(IPM17_BREAK) || res > T(1e-9)) st = MPCB_STATUS_QP_FAIL;
+        if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
         done = true;
       }
       if (!done && valid && ilane) {

@@ -331,3 +331,26 @@ def test_full17_phase_timing_events():
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert t['nominal'] > 0 and t['riccati'] > 0 and t['linearise'] > 0
+
+
+def test_solve17_fp32_input_box_close_to_fp64_oracle():
+    """fp32 interior point on the input box (tolerances scaled to fp32: mu <= 1e-6, residual
+    <= 1e-5): every instance converges and u0 stays within 1e-3 (relative to max(1, |u|)) of
+    the fp64 oracle.  The state box needs fp64 (mpcb_create refuses it in fp32)."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig, _lib
+    N, B = 20, 24
+    x0, xref, uref, p = _inputs(B, N, 31)
+    m = BatchedMPC(MPCConfig.full(N=N, dtype='f32', lbu=LBU17, ubu=UBU17), max_batch=B)
+    m.set_params(p)
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N, lbu=LBU17, ubu=UBU17), p)
+    assert (o['status'] == 0).all()
+    st = m.get_status().cpu().numpy()
+    e = relerr(m.get_control().cpu().numpy().astype(np.float64), o['u0']).max()
+    print(f'17/6 fp32 input box: u0 err {e:.2e}, status {np.bincount(st)}')
+    assert (st == 0).all()
+    assert e <= 1e-3
+    with pytest.raises(_lib.MpcbError, match='f64'):
+        BatchedMPC(MPCConfig.full(N=N, dtype='f32', lbu=LBU17, ubu=UBU17, lbx=-np.ones(17), ubx=np.ones(17)),
+                   max_batch=B)
