@@ -44,6 +44,9 @@ class blasterModel:  # noqa: N801  (reference class name)
         """statesBound as the 17/6 state box (needs the input box too, as the device does)."""
         sb = self._statesBound
         if sb.shape == (2, NX17) and np.isfinite(sb).all() and self._controlBound.size > 0:
+            if self._dtype != 'f64':
+                warnings.warn('statesBound needs dtype f64 on the device; not applied in fp32', stacklevel=3)
+                return {}
             return dict(lbx=sb[0].copy(), ubx=sb[1].copy())
         return {}
 
