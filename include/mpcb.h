@@ -59,7 +59,7 @@ typedef struct mpcb_config {
   int32_t box_u;         /* 1: lbu <= u <= ubu on stages 0..N-1 (idxbu, blastermodel.py:261) */
   int32_t max_as_iter;   /* active-set / interior-point iteration cap for box_u */
   int32_t box_x;         /* 17/6 only, needs box_u: lbx <= x_k <= ubx on stages 1..N-1 (idxbx,
-                            blastermodel.py:255-258 statesBound; JSON constraints.lbx/ubx) */
+                            blastermodel.py:268-270 statesBound; JSON constraints.lbx/ubx) */
   int32_t reserved;
   double dt;             /* Tf / N (solver_options.tf, blastermodel.py:287) */
   double cost_scale;     /* stage-cost scaling; acados uses time_steps[k] = dt */

@@ -97,7 +97,7 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     lbx = ubx = None
     if idxbx:
         # the device's state box covers every state (the reference sets idxbx = range(nx),
-        # blastermodel.py:267) of the 17/6 model, together with the input box
+        # blastermodel.py:268) of the 17/6 model, together with the input box
         if (not slice_12_4 and nx == NX17 and sorted(idxbx) == list(range(nx)) and lbu is not None
                 and np.isfinite(con['lbx']).all() and np.isfinite(con['ubx']).all()):
             lbx = np.empty(nx)

@@ -4,7 +4,7 @@ Same signature and call sequence as the reference:
 ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
 controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
 ``full_model=True`` keeps the reference's 17/6 model, its weights, its input box (controlBound:
-thrusts and swivel rates) and its state box (statesBound, stages 1..N-1, blastermodel.py:267-269)
+thrusts and swivel rates) and its state box (statesBound, stages 1..N-1, blastermodel.py:268-270)
 unchanged — the device's 17/6 path; a statesBound with non-finite entries leaves the state box
 off.  The default keeps the 12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4],
 thrust bounds controlBound[:, :4]; there statesBound is accepted but not enforced.

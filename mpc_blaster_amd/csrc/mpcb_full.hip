@@ -500,7 +500,7 @@ constexpr double IPM17_TOL_F32 = 1e-6, IPM17_BREAK_F32 = 1e-3, IPM17_RES_F32 = 1
 // gradient - sigma mu (1/s_l - 1/s_u)), a common primal/dual step length tau to the boundary,
 // until mu = mean(lambda s) <= 1e-12 (or a breakdown of the Newton system once mu <= 1e-8).  (The exact active set of the 12/4 path needs thousands of
 // exchanges on this model: the swivel-rate weight is 1e-5.)  With a.sbox also the state box
-// lbx <= x_k <= ubx on stages 1..N-1 (blastermodel.py:255-258): explicit slacks and multipliers
+// lbx <= x_k <= ubx on stages 1..N-1 (blastermodel.py:268-270): explicit slacks and multipliers
 // per row (workspace IX, owned by the state lane), an infeasible start, barrier terms on the
 // diagonal of H_xx, and convergence also needs max |r| <= 1e-9.
 template <class T, bool BOX>
