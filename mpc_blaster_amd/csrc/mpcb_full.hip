@@ -194,10 +194,74 @@ __device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>
   }
 }
 
+// The workspace linearisation packs 4 (instance, stage) pairs per wavefront, 16 lanes each:
+// lanes 0..13 integrate the tangents that need the RK4 (Euler angles, body rates, swivel
+// angles, the six inputs); lanes 14 / 15 write the 9 constant columns.  f does not depend on
+// the position or POC states (column e_j), and it is linear in the velocity with a constant
+// Jacobian (dk_1 = .. = dk_4 = c = e_pos + Jp e_v in the POC rows, so RK4 gives e_j + h c).
+constexpr int LQ17 = 16, GQ17 = 64 / LQ17;
 template <class T>
 __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
-  lin17_body<T, true>(a.nb, a.N, a.h, a.M, a.p ? a.p : a.W->p, a.p ? a.p_sb : 0, nullptr, nullptr,
-                      a.b0, a.ws, a.mode, nullptr, nullptr, nullptr);
+  const int lane = threadIdx.x;
+  const int t = lane % LQ17;
+  const int N = a.N;
+  const int64_t idx = (int64_t)blockIdx.x * GQ17 + lane / LQ17;   // (instance, stage) pair
+  if (idx >= a.nb * N) return;
+  const int64_t c = idx / N;
+  const int k = (int)(idx % N);
+  const int64_t b = a.b0 + c;
+  const T* pb = a.p ? a.p + b * a.p_sb : a.W->p;
+  Ws17<T> w(a.ws + c * full17_elems(N), N);
+  T* ABk = w.AB + (int64_t)k * NZ17 * NX17;
+  if (t >= 14) {
+    if (t == 14) {   // position and POC-state directions
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int jj = q < 3 ? q : 11 + q;
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) ABk[jj * NX17 + i] = (i == jj) ? T(1) : T(0);
+      }
+    } else {         // velocity directions
+      P17<T> P;
+      unpack_p17(pb, P);
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        const int jj = 6 + cc;
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) {
+          T v = (i == jj) ? T(1) : T(0);
+          if (i == cc) v = a.h;
+          if (i >= 14) v = a.h * P.Jp[(i - 14) * 3 + cc];
+          ABk[jj * NX17 + i] = v;
+        }
+      }
+    }
+    return;
+  }
+  const int j = t < 3 ? 3 + t : (t < 8 ? 6 + t : 9 + t);   // 3..5, 9..13, 17..22
+  P17<T> P;
+  unpack_p17(pb, P);
+  const T* xk = w.XB + (int64_t)k * NX17;
+  const T* uk = w.UB + (int64_t)k * NU17;
+  T x[NX17], u[NU17], dx[NX17], du[NU17], xn[NX17], col[NX17];
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    x[i] = xk[i];
+    dx[i] = (j == i) ? T(1) : T(0);
+  }
+#pragma unroll
+  for (int m = 0; m < NU17; ++m) {
+    u[m] = uk[m];
+    du[m] = (j == NX17 + m) ? T(1) : T(0);
+  }
+  rk4_17<T, true>(x, dx, u, du, a.h, a.M, P, xn, col);
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) ABk[j * NX17 + i] = col[i];
+  if (t == 0) {   // gap Phi(xbar_k, ubar_k) - xbar_{k+1}; the rollout is gap-free by construction
+#pragma unroll
+    for (int i = 0; i < NX17; ++i)
+      w.GP[(int64_t)k * NX17 + i] = (a.mode == MPCB_MODE_ITERATE) ? xn[i] - xk[NX17 + i] : T(0);
+  }
 }
 
 // ---- phases 1 + 2: Riccati backward over the cached [A|B], then the forward pass -------------
@@ -761,7 +825,7 @@ template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + G17 - 1) / G17)), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + GQ17 - 1) / GQ17)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (a.box)
     hipLaunchKernelGGL((riccati17_kernel<T, true>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
