@@ -92,23 +92,12 @@ def cpu_baseline(w, budget_s=12.0):
                 sample=f'{done} instances of {w["name"]} (N={w["N"]}, fp64, {kind}) in {t_used:.1f} s')
 
 
-def measured_traffic(workload: str):
-    """HBM bytes per Riccati launch from the committed PMC summary (tools/pmc_summary.py)."""
-    p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
-    if not os.path.exists(p):
-        return None
-    try:
-        return json.load(open(p)).get('hbm_bytes_per_riccati_launch')
-    except Exception:
-        return None
-
-
 def run(w, world, rank, dev, steps, warmup):
     import torch
     import torch.distributed as dist
 
     from mpc_blaster_amd import BatchedMPC, MPCConfig
-    from mpc_blaster_amd.dist import allreduce_histogram
+    from mpc_blaster_amd.dist import StepPipeline
     B, N = w['batch'], w['N']
     cfg = MPCConfig(N=N, dtype=w['dtype'], lbu=np.zeros(4) if w['box'] else None,
                     ubu=np.full(4, 65.0) if w['box'] else None, max_as_iter=w.get('max_as_iter', 200))
@@ -123,43 +112,20 @@ def run(w, world, rank, dev, steps, warmup):
                 torch.empty((B, N + 1, 12), dtype=tdt, device=dev) if traj else None,
                 torch.empty((B, N, 4), dtype=tdt, device=dev) if traj else None,
                 torch.zeros((B,), dtype=torch.int32, device=dev))
-    # two output sets: with several ranks the RCCL collective of step i (async, on the process
-    # group's own stream) overlaps the solve of step i+1, which writes the other set; a set is
-    # reused only after its collective has been waited on (the compute stream waits for it)
-    nbuf = 2 if world > 1 else 1
-    out_sets = [make_outs() for _ in range(nbuf)]
-    gathered = [torch.empty((world * B, 4), dtype=tdt, device=dev) for _ in range(nbuf)] \
-        if (world > 1 and traj) else None
-    counts = [torch.zeros((4, 64), dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    pipe = StepPipeline(make_outs, 'histogram' if w['hist'] else 'gather', world,
+                        histogram=lambda u0, counts: mpc.histogram(u0, 0.0, 65.0, 64, counts=counts))
     stream = torch.cuda.current_stream()
-    pending = [None] * nbuf
-    it = [0]
+
+    def solve(o):
+        mpc.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=traj, out=o)
 
     def step(ev=None):
-        i = it[0] % nbuf
-        it[0] += 1
-        if pending[i] is not None:
-            pending[i].wait()
-            pending[i] = None
-        o = out_sets[i]
-        if ev is not None:
-            ev[0].record(stream)
-        mpc.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=traj, out=o)
-        if ev is not None:
-            ev[1].record(stream)
-        if w['hist']:
-            counts[i].zero_()
-            mpc.histogram(o[0], 0.0, 65.0, 64, counts=counts[i])
-            if world > 1:
-                pending[i] = allreduce_histogram(counts[i], async_op=True)
-        elif world > 1:
-            pending[i] = dist.all_gather_into_tensor(gathered[i], o[0], async_op=True)
+        if ev is None:
+            pipe.step(solve)
+        else:
+            pipe.step(solve, before=lambda: ev[0].record(stream), after=lambda: ev[1].record(stream))
 
-    def drain():
-        for i in range(nbuf):
-            if pending[i] is not None:
-                pending[i].wait()
-                pending[i] = None
+    drain = pipe.drain
 
     for _ in range(warmup):
         step()
@@ -179,7 +145,7 @@ def run(w, world, rank, dev, steps, warmup):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    bad = int(sum((o[3] != 0).sum().item() for o in out_sets))
+    bad = pipe.bad_status()
     # per-phase device time (HIP events the library records on the launch stream around each
     # kernel); a separate pass so that reading the events does not serialise the timed region
     mpc.set_timing(True)
@@ -200,10 +166,70 @@ def run(w, world, rank, dev, steps, warmup):
         ph = torch.tensor([phase_ms[k] for k in sorted(phase_ms)], dtype=torch.float64, device=dev)
         dist.all_reduce(ph, op=dist.ReduceOp.MAX)
         phase_ms = dict(zip(sorted(phase_ms), ph.tolist()))
+    qp = None
+    if w['box']:   # active-set work of the last solve: forward passes, masked backward stages
+        st = mpc.qp_stats(B).double().cpu().numpy()
+        qp = dict(fwd_passes=float(st[:, 0].sum()), bwd_stages=float(st[:, 1].sum()),
+                  mean_iters=float(st[:, 0].mean()), max_iters=int(st[:, 0].max()))
+        if world > 1:
+            t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=dev)
+            dist.all_reduce(t)
+            qp['fwd_passes'], qp['bwd_stages'] = float(t[0]) / world, float(t[1]) / world
     path = 'split (3 kernels)' if mpc.path == 'split' else 'fused (1 kernel)'
     mpc.close()
     return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path, phase_ms=phase_ms,
-                split=path.startswith('split'))
+                split=path.startswith('split'), qp=qp)
+
+
+def phase_kernels(w):
+    """rocprof names and algorithmic flop counts of the split path's three launches for this
+    workload (the library picks the variants by chunk size: mpcb_capi.hip mpcb_create).
+    Dense algorithmic counts per shooting interval:
+      nominal  4 f evaluations (4 x 300) of the RK4 rollout;
+      riccati  RK4 sensitivities minus those f evaluations plus the Riccati backward
+               (21,996 - 1,200 + 12,309 = 33,105);
+      forward  du = K dx + k, dx' = [A|B] (dx, du) (+ gap): 480;
+      box      the active-set kernel (c4): per masked backward stage recomputed 12,309 (the Riccati
+               algebra over the cached [A|B]), per forward stage 480 + the multipliers
+               mu = G_u (dx, du) + h_u (2 x 17 x 4 = 136), counted from the kernel's own per-instance
+               statistics (mpcb_qp_stats) rather than assumed.
+    """
+    t = 'float' if w['dtype'] == 'f32' else 'double'
+    small = w['batch'] <= 16384
+    names = {'nominal': f'nominal_quad_kernel<{t}>' if small else f'nominal_kernel<{t}>',
+             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}>'}
+    if w['box']:
+        names['forward'] = f'box_kernel_{w["dtype"]}<1>'
+    elif not w['hist']:
+        names['forward'] = f'box_kernel_{w["dtype"]}<2>' if small else f'forward_kernel<{t}, false>'
+    return names
+
+
+def kernel_flops(w, r, phase):
+    B, N = w['batch'], w['N']
+    if phase == 'nominal':
+        return 1200 * N * B
+    if phase == 'riccati':
+        return FLOP_PER_INTERVAL_RICCATI * N * B
+    if w['box']:
+        q = r['qp']
+        return 12309 * q['bwd_stages'] + (480 + 136) * N * q['fwd_passes']
+    return 480 * N * B
+
+
+def pmc_kernel(workload: str, kernel: str):
+    """Counter-derived figures of one kernel from the committed PMC summary (tools/pmc_summary.py)."""
+    p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
+    if not os.path.exists(p):
+        return None
+    try:
+        per = json.load(open(p)).get('per_kernel', {})
+    except Exception:
+        return None
+    for k, v in per.items():
+        if k.endswith('::' + kernel) or k == kernel:
+            return v
+    return None
 
 
 def summarize(w, r, world, steps):
@@ -211,29 +237,44 @@ def summarize(w, r, world, steps):
     value = B * world * steps / r['elapsed']
     peak = PEAK_TFLOPS[w['dtype']]
     ph = r['phase_ms']
-    per_interval = FLOP_PER_INTERVAL_RICCATI if r['split'] else FLOP_PER_INTERVAL
-    achieved_tf = per_interval * N * B / (ph['riccati'] * 1e-3) / 1e12
-    solve_tf = FLOP_PER_INTERVAL * N * B / (r['kern_ms'] * 1e-3) / 1e12
+    if not r['split']:
+        raise RuntimeError('bench expects the split path')
+    names = phase_kernels(w)
+    # the dominant kernel by device time (HIP events on its launch stream)
+    dom = max(names, key=lambda k: ph.get(k, 0.0))
+    flop = kernel_flops(w, r, dom)
+    achieved_tf = flop / (ph[dom] * 1e-3) / 1e12
+    solve_flop = sum(kernel_flops(w, r, k) for k in names)
+    solve_tf = solve_flop / (r['kern_ms'] * 1e-3) / 1e12
     hbm_gbs = compulsory_bytes(w) * B / (r['kern_ms'] * 1e-3) / 1e9
-    roof = {'bound': 'mfma', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': achieved_tf / peak, 'traffic': measured_traffic(w['name']),
-            'kernel': 'riccati_kernel_%s' % w['dtype'] if r['split'] else 'solve (single launch)',
-            'kernel_ms': ph['riccati'],
-            'flop_per_launch': per_interval * N * B,
-            'phase_ms': ph,
+    pk = pmc_kernel(w['name'], names[dom]) or {}
+    ex = pk.get('executed_flops_per_launch')
+    roof = {'bound': 'valu', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': achieved_tf / peak, 'traffic': pk.get('hbm_bytes_per_launch'),
+            'kernel': names[dom], 'kernel_ms': ph[dom],
+            'flop_per_launch': flop,
+            'executed_frac': (ex / (ph[dom] * 1e-3) / 1e12 / peak) if ex else None,
+            'phase_ms': ph, 'phase_kernels': names,
+            'phase_frac': {k: kernel_flops(w, r, k) / (ph[k] * 1e-3) / 1e12 / peak
+                           for k in names if ph.get(k, 0) > 0},
             'solve_ms': r['kern_ms'],
             'solve_achieved': solve_tf,
             'solve_frac': solve_tf / peak,
             'hbm_compulsory_GBs': hbm_gbs,
             'hbm_frac': hbm_gbs / HBM_PEAK_GBS,
-            'note': ('compute-bound path (SURVEY §8d: ~300-700 flop per compulsory byte). '
-                     f'Dominant kernel = Riccati pass: {per_interval} algorithmic flop per interval '
-                     '(dense count, §8d, minus the nominal f evaluations done by the rollout kernel) '
-                     'x N x B per launch, over its device time from HIP events on its launch stream. '
-                     f'solve_* = the whole solve ({FLOP_PER_INTERVAL} flop/interval) over all its '
-                     'kernels. peak = dense fp64/fp32 rate (gfx950 VALU and MFMA peaks are equal). '
-                     'traffic = HBM bytes per Riccati launch from PMC FETCH_SIZE x 2 + WRITE_SIZE '
-                     '(profiles/pmc_<workload>.json)')}
+            'note': ('compute-bound path (SURVEY §8d: ~300-700 flop per compulsory byte), executed '
+                     'on the vector ALUs (fp64: DPP row-broadcast v_fmac_f64; fp32: VALU plus '
+                     'v_mfma_f32_16x16x1_4b outer products; on gfx950 the fp32/fp64 VALU and MFMA '
+                     'peaks are equal). kernel = the launch with the most device time (HIP events '
+                     'on its launch stream); achieved = its dense algorithmic flops (bench.py '
+                     'phase_kernels docstring) / that time. executed_frac = counter-executed flops '
+                     '(64 x SQ_INSTS_VALU_FLOPS_FP32/FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F32, '
+                     'profiles/pmc_<workload>.json) over the same time. traffic = HBM bytes per '
+                     'launch of that kernel, (2 x FETCH_SIZE + WRITE_SIZE) from the same PMC run '
+                     '(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md). solve_* = every kernel '
+                     'of the solve over the whole solve time.')}
+    if r.get('qp'):
+        roof['active_set'] = r['qp']
     return value, roof
 
 

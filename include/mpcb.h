@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MPCB_ABI_VERSION 3
+#define MPCB_ABI_VERSION 4
 
 enum { MPCB_F64 = 0, MPCB_F32 = 1 };
 enum { MPCB_MODE_ROLLOUT = 0, MPCB_MODE_ITERATE = 1 };
@@ -156,14 +156,30 @@ int mpcb_gen_inputs(mpcb_handle* h, int64_t B, uint64_t seed, uint64_t id_offset
                     void* wind, void* hip_stream);
 
 /*
- * Model parameters of the full 17/6 model (nx == 17): acados ``ocp_solver.set(k, 'p', p)`` /
- * ``integrator.set('p', p)`` (simulation_blaster.py:69, blastermodel.py:203-210), the same
- * vector on every stage.  ``params`` is a DEVICE array [B|1, 25] (column-major vec of
- * J_angles 3x2, J_euler 3x3, J_p 3x3, then T_blast) that the caller keeps alive for the later
- * solve / linearize / sim_step calls; stride 0 broadcasts; NULL restores the defaults
- * (zeros, T_blast = cfg.t_blast).  MPCB_E_UNSUPPORTED on a 12/4 handle.
+ * Model parameters of the full 17/6 model (nx == 17): acados ``ocp_solver.set(k, 'p', p)``,
+ * stage by stage (simulation_blaster.py:65-69; the vector layout of blastermodel.py:203-210:
+ * column-major vec of J_angles 3x2, J_euler 3x3, J_p 3x3, then T_blast).
+ *   params     DEVICE array; the 25-vector of instance b at stage k starts at
+ *              params[b * params_sb + k * params_kb] (elements).  params_sb == 0: one row for
+ *              every instance; params_kb == 0: the same vector on every stage 0..N-1 (the
+ *              terminal stage has no dynamics).  mpcb_sim_step reads stage 0.
+ *   count      instance rows the array holds: a later solve / linearize / sim_step of B > count
+ *              instances fails with MPCB_E_INVALID unless params_sb == 0.
+ * The caller keeps the array alive for those later calls.  NULL restores the defaults (zeros,
+ * T_blast = mpcb_set_t_blast / cfg.t_blast, acados ``parameter_values``, blastermodel.py:280-282).
+ * MPCB_E_UNSUPPORTED on a 12/4 handle (its only parameter is T_blast: mpcb_set_t_blast).
  */
-int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb);
+int mpcb_set_params(mpcb_handle* h, int64_t count, const void* params, int64_t params_sb,
+                    int64_t params_kb);
+
+/*
+ * T_blast, the blaster thrust p[24] (blastermodel.py:210), as a host scalar.  12/4 model: the
+ * body-z force of the rigid-body slice for every instance and stage of later calls (replaces
+ * ``set(k, 'p', p)`` with the Jacobian blocks zero; no re-creation of the handle).  17/6 model:
+ * the default parameter vector's p[24] (used while no device parameters are set).  Waits for the
+ * device (a configuration call, not a per-step one).
+ */
+int mpcb_set_t_blast(mpcb_handle* h, double t_blast);
 
 /*
  * Point-of-contact Jacobians of the blaster stream for B vehicle poses (fp64, runs on the
@@ -180,6 +196,16 @@ int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb);
 int mpcb_poc_jacobians(int64_t B, const double* pose, double stream_velocity, const double* Mc,
                        int max_iter, double t_blast, double* poc, double* J_eul, double* J_mot,
                        double* J_pos, double* p25, int32_t* status, void* hip_stream);
+
+/*
+ * Work statistics of the last solve on a 12/4 input-box handle (the active-set QP, c4): per
+ * instance ``out[2b]`` = forward passes until its active set was the KKT point (including the
+ * first, after the unconstrained Riccati pass) and ``out[2b+1]`` = backward stages its masked
+ * Riccati passes recomputed (restarts skip the stages above the highest changed one).  ``out``
+ * is a DEVICE int32 array [B, 2], B <= that solve's batch.  No reference counterpart (HPIPM's
+ * ``get_stats('qp_iter')``).  MPCB_E_UNSUPPORTED on other handles.
+ */
+int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* hip_stream);
 
 /* Histogram of u0 per input channel over [lo, hi) into counts[nu][nbins] (int64, accumulated). */
 int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,

@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = 'libmpcblaster.so'
 LIB_PATH = os.path.join(_HERE, LIB_NAME)
 
+ABI_VERSION = 4
 MPCB_F64, MPCB_F32 = 0, 1
 MPCB_MAX_NX, MPCB_MAX_NU = 17, 6
 STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
@@ -19,7 +20,7 @@ STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram', 'mpcb_set_timing',
-           'mpcb_last_timing', 'mpcb_set_params', 'mpcb_poc_jacobians')
+           'mpcb_last_timing', 'mpcb_set_params', 'mpcb_set_t_blast', 'mpcb_qp_stats', 'mpcb_poc_jacobians')
 
 
 class MpcbConfig(ctypes.Structure):
@@ -78,7 +79,9 @@ def load(path: str | None = None):
     lib.mpcb_histogram.argtypes = [vp, i64, vp, dbl, dbl, i32, vp, vp]
     lib.mpcb_set_timing.argtypes = [vp, i32]
     lib.mpcb_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
-    lib.mpcb_set_params.argtypes = [vp, vp, i64]
+    lib.mpcb_set_params.argtypes = [vp, i64, vp, i64, i64]
+    lib.mpcb_set_t_blast.argtypes = [vp, dbl]
+    lib.mpcb_qp_stats.argtypes = [vp, i64, vp, vp]
     lib.mpcb_poc_jacobians.argtypes = [i64, vp, dbl, ctypes.POINTER(dbl), i32, dbl, vp, vp, vp, vp, vp,
                                        vp, vp]
     for name in EXPORTS:

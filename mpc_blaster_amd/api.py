@@ -161,16 +161,49 @@ class BatchedMPC:
         return self._u0
 
     def set_params(self, p):
-        """Parameters of the full 17/6 model, [B|1, 25] (acados ``set(k, 'p', p)``,
-        simulation_blaster.py:69): column-major J_angles 3x2, J_euler 3x3, J_p 3x3, T_blast.
-        ``None`` restores the defaults (zeros, T_blast = config.t_blast)."""
+        """Parameters of the full 17/6 model (acados ``set(k, 'p', p)``,
+        simulation_blaster.py:65-69): column-major J_angles 3x2, J_euler 3x3, J_p 3x3, T_blast.
+
+        Shapes: [25] or [B|1, 25] (every stage alike), or [B|1, N|N+1, 25] stage by stage (the
+        terminal stage N has no dynamics; its row is ignored).  ``None`` restores the defaults
+        (zeros, T_blast = ``config.t_blast`` / ``set_t_blast``)."""
+        if self.nx != 17:
+            raise ValueError('set_params is for the 17/6 model; the 12/4 slice takes set_t_blast')
         if p is None:
             self._params = None
-            _lib.check(self.lib.mpcb_set_params(self._h, ctypes.c_void_p(0), 0))
+            _lib.check(self.lib.mpcb_set_params(self._h, 0, ctypes.c_void_p(0), 0, 0))
             return
-        t, sb = self._dev(p, (25,), 'p')
+        torch = _torch()
+        N = self.cfg.N
+        t = torch.as_tensor(p, dtype=self.dtype, device=f'cuda:{self.device}')
+        if t.dim() == 1:
+            t = t.reshape(1, 1, -1)
+        elif t.dim() == 2:
+            t = t.unsqueeze(1)
+        if t.dim() != 3 or t.shape[-1] != 25 or t.shape[1] not in (1, N, N + 1):
+            raise ValueError(f'p: expected [25], [B|1, 25] or [B|1, N|N+1, 25], got {tuple(p.shape)}')
+        t = t.contiguous()
         self._params = t   # the library keeps the device pointer: hold the tensor
-        _lib.check(self.lib.mpcb_set_params(self._h, self._ptr(t), 0 if t.shape[0] == 1 else 25))
+        rows, stages = t.shape[0], t.shape[1]
+        sb = 0 if rows == 1 else stages * 25
+        kb = 0 if stages == 1 else 25
+        _lib.check(self.lib.mpcb_set_params(self._h, rows, self._ptr(t), sb, kb))
+
+    def set_t_blast(self, t_blast: float):
+        """Blaster thrust p[24] (blastermodel.py:210) as a scalar for every instance and stage:
+        the 12/4 slice's body-z force; on the 17/6 model the default parameter vector's T_blast.
+        Updates the handle in place (no re-creation)."""
+        _lib.check(self.lib.mpcb_set_t_blast(self._h, float(t_blast)))
+        self.cfg.t_blast = float(t_blast)
+
+    def qp_stats(self, B=None):
+        """Input-box (12/4) work statistics of the last solve: int32 [B, 2] device tensor of
+        (forward passes, masked backward stages) per instance (mpcb_qp_stats)."""
+        torch = _torch()
+        B = self._u0.shape[0] if B is None else int(B)
+        out = torch.empty((B, 2), dtype=torch.int32, device=f'cuda:{self.device}')
+        _lib.check(self.lib.mpcb_qp_stats(self._h, B, self._ptr(out), self._stream()))
+        return out
 
     def get_control(self):
         """First-step control u0* of the last solve, [B,4] device tensor."""

@@ -28,17 +28,30 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, out: str | None = None, extra=()) -> str:
-    out = out or OUT
-    if out == OUT and not force and not needs_build():
-        return OUT
-    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', out + '.tmp']
+def _run(cmd, verbose):
     if verbose:
         print('[mpcb build]', ' '.join(shlex.quote(c) for c in cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError(f'hipcc failed ({r.returncode})')
+        raise RuntimeError(f'hipcc failed ({r.returncode}): {cmd[-1]}')
+
+
+def build(force: bool = False, verbose: bool = True, out: str | None = None, extra=()) -> str:
+    """One hipcc -c per translation unit (in parallel), then one shared-object link."""
+    from concurrent.futures import ThreadPoolExecutor
+    out = out or OUT
+    if out == OUT and not force and not needs_build():
+        return OUT
+    objdir = out + '.objs'
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f for f in FLAGS if f != '-shared'] + list(extra)
+    objs = [os.path.join(objdir, os.path.splitext(s)[0] + '.o') for s in SOURCES]
+    cmds = [[HIPCC] + flags + ['-c', os.path.join(CSRC, s), '-o', o] for s, o in zip(SOURCES, objs)]
+    jobs = max(1, min(len(cmds), int(os.environ.get('MAX_JOBS', '8'))))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), cmds))
+    _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}'] + objs + ['-o', out + '.tmp'], verbose)
     os.replace(out + '.tmp', out)
     return out
 

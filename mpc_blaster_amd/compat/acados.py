@@ -86,6 +86,11 @@ class AcadosOcpSolver:
         self._lbx0 = None
         self.yref = np.zeros((self.B, N + 1, NX + NU))
         self.status = np.zeros(self.B, dtype=np.int32)
+        # acados parameter_values per stage (blastermodel.py:280-282: zeros, T_blast = p[24]);
+        # uploaded at the next solve() when a set(k, 'p') changed them
+        self._p = np.zeros((self.B, N + 1, 25))
+        self._p[..., 24] = config.t_blast
+        self._p_dirty = False
 
     @property
     def N(self):
@@ -110,25 +115,35 @@ class AcadosOcpSolver:
         elif field == 'u':
             self.ubar[:, stage] = torch.as_tensor(_slice_u(value, self.B, 'u', self.nu),
                                                   dtype=self.ubar.dtype, device=self._dev)
-        elif field == 'p' and self.nx == NX_REF:
-            # the same vector on every stage (the reference scripts set all stages alike)
-            self.mpc.set_params(_as_batch(value, 25, self.B, 'p'))
         elif field == 'p':
-            p = np.asarray(value, dtype=np.float64).reshape(-1)
-            if p.size == 25 and p[24] != self.cfg.t_blast:
-                # T_blast (blastermodel.py:203-210, p[24]) enters the 12/4 slice as a body-z force
-                self._set_t_blast(float(p[24]))
-            if p.size == 25 and np.any(p[:24] != 0):
-                warnings.warn('POC Jacobian parameters only affect the POC states, which the 12/4 '
-                              'model does not carry; ignored', stacklevel=2)
+            if not 0 <= stage <= self.N:
+                raise IndexError(f'stage {stage} outside 0..{self.N}')
+            self._p[:, stage] = _as_batch(value, 25, self.B, 'p')
+            self._p_dirty = True
         else:
             raise KeyError(f'field {field!r} not supported')
 
-    def _set_t_blast(self, t):
-        from ..api import BatchedMPC
-        self.cfg.t_blast = t
-        self.mpc.close()
-        self.mpc = BatchedMPC(self.cfg, max_batch=self.B, device=self.mpc.device)
+    def _upload_params(self):
+        """Hand the per-stage parameters to the device (acados keeps p per stage; the terminal
+        stage has no dynamics, so stages 0..N-1 are what the solve reads)."""
+        self._p_dirty = False
+        p = self._p[:, :self.N]
+        if self.nx == NX_REF:
+            same_stages = bool(np.all(p == p[:, :1]))
+            same_rows = bool(np.all(p == p[:1]))
+            self.mpc.set_params(p[:1, 0] if (same_stages and same_rows) else
+                                (p[:, 0] if same_stages else p))
+            return
+        # 12/4 slice: T_blast (p[24]) is the model's only parameter there, a handle scalar
+        t = p[..., 24]
+        if not np.all(t == t.flat[0]):
+            raise NotImplementedError('the 12/4 slice takes one T_blast for every instance and stage '
+                                      '(stage- or instance-varying p[24] needs the 17/6 model)')
+        if np.any(p[..., :24] != 0):
+            warnings.warn('POC Jacobian parameters only affect the POC states, which the 12/4 '
+                          'model does not carry; ignored', stacklevel=3)
+        if float(t.flat[0]) != self.cfg.t_blast:
+            self.mpc.set_t_blast(float(t.flat[0]))
 
     def cost_set(self, stage: int, field: str, value):
         if field != 'yref':
@@ -141,6 +156,8 @@ class AcadosOcpSolver:
     # -------------------------------------------------------------- solve
     def solve(self) -> int:
         torch = _torch()
+        if self._p_dirty:
+            self._upload_params()
         xr = self.yref[:, :, :self.nx]
         ur = self.yref[:, :self.N, self.nx:]
         self.mpc.solve_iterate(self.x0, self.xbar, self.ubar, xr, ur,
@@ -197,15 +214,15 @@ class AcadosSimSolver:
             self.x = _slice_x(value, self.B, 'x', self.nx).copy()
         elif field == 'u':
             self.u = _slice_u(value, self.B, 'u', self.nu).copy()
-        elif field == 'p' and self.nx == NX_REF:
-            self.mpc.set_params(_as_batch(value, 25, self.B, 'p'))
         elif field == 'p':
-            p = np.asarray(value, dtype=np.float64).reshape(-1)
-            if p.size == 25 and p[24] != self.cfg.t_blast:
-                from ..api import BatchedMPC
-                self.cfg.t_blast = float(p[24])
-                self.mpc.close()
-                self.mpc = BatchedMPC(self.cfg, max_batch=self.B, device=self.mpc.device)
+            p = _as_batch(value, 25, self.B, 'p')
+            if self.nx == NX_REF:
+                self.mpc.set_params(p[:1] if np.all(p == p[:1]) else p)
+            else:
+                if not np.all(p[:, 24] == p[0, 24]):
+                    raise NotImplementedError('the 12/4 slice takes one T_blast for every instance')
+                if float(p[0, 24]) != self.cfg.t_blast:
+                    self.mpc.set_t_blast(float(p[0, 24]))
         elif field == 'T':
             self.T = float(value)
         else:

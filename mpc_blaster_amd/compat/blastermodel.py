@@ -18,6 +18,9 @@ import numpy as np
 from ..config import NU, NU17, NX, NX17, MPCConfig
 from .acados import AcadosOcpSolver, AcadosSimSolver
 
+# acados parameter_values[24] of generateController (blastermodel.py:280-282; JSON :3423)
+DEFAULT_T_BLAST = 2.2 * 9.81
+
 
 class blasterModel:  # noqa: N801  (reference class name)
     def __init__(self, mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
@@ -54,13 +57,14 @@ class blasterModel:  # noqa: N801  (reference class name)
         """Builds the problem definition (the dynamics themselves live in the HIP kernels)."""
         cb = self._controlBound
         if self._full:
-            # generateController's default parameter vector: T_blast = blastThruster * 9.81
-            # (blastermodel.py:280-282); the rest of p is set per stage by the scripts
+            # generateController's default parameter vector: zeros and T_blast = 2.2 * 9.81,
+            # hard-coded whatever blastThruster is (blastermodel.py:280-282); the scripts then
+            # set p stage by stage (simulation_blaster.py:65-69)
             self._cfg = MPCConfig(
                 N=self._N, dt=self._Tf / self._N, dtype=self._dtype, mass=self._M, J=self._J,
                 lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
                 Q=self._Q_weight[:NX17, :NX17], R=self._R_weight[:NU17, :NU17],
-                QN=self._Q_weight_t[:NX17, :NX17], t_blast=self._blastThruster * 9.81,
+                QN=self._Q_weight_t[:NX17, :NX17], t_blast=DEFAULT_T_BLAST,
                 nx=NX17, nu=NU17,
                 lbu=cb[0][:NU17] if cb.size else None, ubu=cb[1][:NU17] if cb.size else None,
                 **self._state_box())
@@ -70,9 +74,9 @@ class blasterModel:  # noqa: N801  (reference class name)
             lx=self._arm_length_x, ly=self._arm_length_y, c=self._c,
             Q=self._Q_weight[:NX, :NX], R=self._R_weight[:NU, :NU], QN=self._Q_weight_t[:NX, :NX],
             lbu=cb[0][:NU], ubu=cb[1][:NU],
-            # default parameter vector of generateController (blastermodel.py:280-282) has
-            # T_blast = 2.2*9.81; the 12/4 quad configs use p[24] = 0 unless set(k,'p',...)
-            t_blast=0.0)
+            # the same default parameter vector (blastermodel.py:280-282): T_blast = 2.2 * 9.81
+            # until set(k, 'p', p) changes it (a quad without the blaster sets p[24] = 0)
+            t_blast=DEFAULT_T_BLAST)
         return 0
 
     def generateController(self):

@@ -74,6 +74,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
   bool done = false;
   int32_t st = MPCB_STATUS_OK;
   int best = 0x7fffffff, pcount = 3;
+  int n_fwd = 0, n_bst = 0;   // this instance's forward passes / masked backward stages (qp_stats)
 
   // Stages above the highest stage whose active set changed keep their gains: each backward
   // pass restarts at kc (group-uniform; N - 1 on the first masked pass) from the value function
@@ -88,6 +89,8 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       const int o = __shfl(kc, g * 16);
       kmax = o > kmax ? o : kmax;
     }
+    if (BOX && it > 0 && !done && kc >= 0) n_bst += kc + 1;
+    if (BOX && !done) ++n_fwd;
     if ((BOX ? it > 0 : MODE == PASS_SMALL) && kmax >= 0) {
       T pj = T(0);
       T Pc[NX];
@@ -457,6 +460,10 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     // the QP status of the unconstrained pass (P2 wrote it) carries over
     const int32_t st0 = MODE != PASS_SMALL ? a.status[b] : MPCB_STATUS_OK;
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
+    if (BOX && a.qp_stats) {
+      a.qp_stats[2 * b] = n_fwd;
+      a.qp_stats[2 * b + 1] = n_bst;
+    }
   }
 }
 

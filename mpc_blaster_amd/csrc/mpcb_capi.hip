@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <string>
 
@@ -79,8 +80,21 @@ struct mpcb_handle {
   // the defaults in the weights block), chunk of instances per launch
   int full = 0;
   const void* params = nullptr;
-  int64_t params_sb = 0;
+  int64_t params_sb = 0, params_kb = 0;
+  int64_t params_count = 0;   // instance rows behind params (checked against B when params_sb != 0)
+  int32_t* qp_stats = nullptr;   // 12/4 input box: per instance [forward passes, masked stages]
+  int64_t qp_stats_rows = 0;     // instances of the last boxed solve
 };
+
+// A 17/6 call over B instances may only read parameter rows that exist (mpcb_set_params count).
+static int check_params(const mpcb_handle* h, int64_t B) {
+  if (h->full && h->params && h->params_sb != 0 && B > h->params_count) {
+    g_err = "batch " + std::to_string(B) + " exceeds the " + std::to_string(h->params_count) +
+            " parameter rows given to mpcb_set_params";
+    return MPCB_E_INVALID;
+  }
+  return MPCB_OK;
+}
 
 extern "C" const char* mpcb_last_error(void) { return g_err.c_str(); }
 extern "C" int mpcb_abi_version(void) { return MPCB_ABI_VERSION; }
@@ -273,6 +287,15 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     delete h;
     return fail(MPCB_E_HIP, "weights upload: %s", hipGetErrorString(e));
   }
+  if (!full && h->split && cfg->box_u) {
+    e = hipMalloc((void**)&h->qp_stats, (size_t)max_batch * 2 * sizeof(int32_t));
+    if (e != hipSuccess) {
+      (void)hipFree(h->scratch);
+      (void)hipFree(h->weights);
+      delete h;
+      return fail(MPCB_E_NOMEM, "qp stats: %s", hipGetErrorString(e));
+    }
+  }
   *out = h;
   return MPCB_OK;
 }
@@ -285,7 +308,22 @@ extern "C" int mpcb_destroy(mpcb_handle* h) {
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(h->scratch);
   (void)hipFree(h->weights);
+  if (h->qp_stats) (void)hipFree(h->qp_stats);
   delete h;
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* stream) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (!h->qp_stats) return fail(MPCB_E_UNSUPPORTED, "QP statistics are kept by the 12/4 input-box path");
+  if (B < 0 || B > h->qp_stats_rows)
+    return fail(MPCB_E_INVALID, "batch %lld exceeds the last boxed solve's %lld instances", (long long)B,
+                (long long)h->qp_stats_rows);
+  if (B == 0) return MPCB_OK;
+  if (!out) return fail(MPCB_E_INVALID, "null array");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpyAsync(out, h->qp_stats, (size_t)B * 2 * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
   return MPCB_OK;
 }
 
@@ -303,7 +341,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.s = (T)h->cfg.cost_scale;
     if constexpr (sizeof(T) == 8) a.M = h->Md; else a.M = h->Mf;
     a.W = reinterpret_cast<const Weights17<T>*>(h->weights);
-    a.p = (const T*)h->params; a.p_sb = h->params_sb;
+    a.p = (const T*)h->params; a.p_sb = h->params_sb; a.p_kb = h->params_kb;
     a.x0 = (const T*)x0; a.x0_sb = x0_sb;
     a.xref = (const T*)xref; a.xref_sb = xref_sb;
     a.uref = (const T*)uref; a.uref_sb = uref_sb;
@@ -362,6 +400,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
+      a.qp_stats = h->qp_stats;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));
@@ -371,6 +410,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       h->timed_chunks = chunk_i < mpcb_handle::TCHUNKS ? chunk_i : mpcb_handle::TCHUNKS;
       h->timed_split = 1;
     }
+    if (h->qp_stats) h->qp_stats_rows = B;
     return MPCB_OK;
   }
   SolveArgs<T> a;
@@ -454,6 +494,7 @@ extern "C" int mpcb_solve(mpcb_handle* h, int64_t B, const void* x0, int64_t x0_
                int64_t xref_sb, const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                void* u0, void* X, void* U, int32_t* status, void* stream) {
   int rc = check_solve(h, B, x0, xref, uref, u0, X, U, status);
+  if (!rc) rc = check_params(h, B);
   if (rc || B == 0) return rc;
   HIP_TRY(hipSetDevice(h->device));
   if (h->cfg.dtype == MPCB_F64)
@@ -468,6 +509,7 @@ extern "C" int mpcb_solve_iterate(mpcb_handle* h, int64_t B, const void* x0, int
                        int64_t uref_sb, const void* wind, int64_t wind_sb, void* u0, void* X, void* U,
                        int32_t* status, void* stream) {
   int rc = check_solve(h, B, x0, xref, uref, u0, X, U, status);
+  if (!rc) rc = check_params(h, B);
   if (rc || B == 0) return rc;
   if (!xbar || !ubar) return fail(MPCB_E_INVALID, "xbar and ubar are required");
   HIP_TRY(hipSetDevice(h->device));
@@ -484,19 +526,20 @@ extern "C" int mpcb_linearize(mpcb_handle* h, int64_t B, const void* xbar, const
   if (B < 0) return fail(MPCB_E_INVALID, "negative batch");
   if (B == 0) return MPCB_OK;
   if (!xbar || !ubar || !A || !Bm || !xnext) return fail(MPCB_E_INVALID, "null array");
+  if (int rc = check_params(h, B)) return rc;
   HIP_TRY(hipSetDevice(h->device));
   hipError_t e;
   if (h->full) {
     if (wind) return fail(MPCB_E_UNSUPPORTED, "wind is a 12/4-model extension");
-    const int64_t psb = h->params ? h->params_sb : 0;
+    const int64_t psb = h->params ? h->params_sb : 0, pkb = h->params ? h->params_kb : 0;
     if (h->cfg.dtype == MPCB_F64) {
       const double* p = h->params ? (const double*)h->params : reinterpret_cast<const Weights17<double>*>(h->weights)->p;
-      e = launch_linearize17<double>(B, h->cfg.N, h->cfg.dt, h->Md, p, psb, (const double*)xbar,
+      e = launch_linearize17<double>(B, h->cfg.N, h->cfg.dt, h->Md, p, psb, pkb, (const double*)xbar,
                                      (const double*)ubar, (double*)A, (double*)Bm, (double*)xnext,
                                      (hipStream_t)stream);
     } else {
       const float* p = h->params ? (const float*)h->params : reinterpret_cast<const Weights17<float>*>(h->weights)->p;
-      e = launch_linearize17<float>(B, h->cfg.N, (float)h->cfg.dt, h->Mf, p, psb, (const float*)xbar,
+      e = launch_linearize17<float>(B, h->cfg.N, (float)h->cfg.dt, h->Mf, p, psb, pkb, (const float*)xbar,
                                     (const float*)ubar, (float*)A, (float*)Bm, (float*)xnext,
                                     (hipStream_t)stream);
     }
@@ -519,6 +562,7 @@ extern "C" int mpcb_sim_step(mpcb_handle* h, int64_t B, const void* x, const voi
   if (B == 0) return MPCB_OK;
   if (!x || !u || !x_out) return fail(MPCB_E_INVALID, "null array");
   if (!(T > 0)) return fail(MPCB_E_INVALID, "T must be > 0");
+  if (int rc = check_params(h, B)) return rc;
   HIP_TRY(hipSetDevice(h->device));
   hipError_t e;
   if (h->full) {
@@ -584,11 +628,37 @@ extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double 
   return MPCB_OK;
 }
 
-extern "C" int mpcb_set_params(mpcb_handle* h, const void* params, int64_t params_sb) {
+extern "C" int mpcb_set_params(mpcb_handle* h, int64_t count, const void* params, int64_t params_sb,
+                               int64_t params_kb) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
-  if (!h->full) return fail(MPCB_E_UNSUPPORTED, "the 12/4 model takes T_blast from the config");
-  if (params_sb < 0) return fail(MPCB_E_INVALID, "negative parameter stride");
+  if (!h->full) return fail(MPCB_E_UNSUPPORTED, "the 12/4 model's only parameter is T_blast (mpcb_set_t_blast)");
+  if (params_sb < 0 || params_kb < 0) return fail(MPCB_E_INVALID, "negative parameter stride");
+  if (params && count < 1) return fail(MPCB_E_INVALID, "parameter rows count=%lld", (long long)count);
   h->params = params;
   h->params_sb = params ? params_sb : 0;
+  h->params_kb = params ? params_kb : 0;
+  h->params_count = params ? count : 0;
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_set_t_blast(mpcb_handle* h, double t_blast) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  if (!std::isfinite(t_blast)) return fail(MPCB_E_INVALID, "T_blast must be finite");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());   // kernels in flight may still read the old value
+  h->cfg.t_blast = t_blast;
+  h->Md.t_blast = t_blast;
+  h->Mf.t_blast = (float)t_blast;
+  if (h->full) {
+    if (h->cfg.dtype == MPCB_F64) {
+      const double v = t_blast;
+      HIP_TRY(hipMemcpy((char*)h->weights + offsetof(Weights17<double>, p) + 24 * sizeof(double), &v,
+                        sizeof(v), hipMemcpyHostToDevice));
+    } else {
+      const float v = (float)t_blast;
+      HIP_TRY(hipMemcpy((char*)h->weights + offsetof(Weights17<float>, p) + 24 * sizeof(float), &v,
+                        sizeof(v), hipMemcpyHostToDevice));
+    }
+  }
   return MPCB_OK;
 }

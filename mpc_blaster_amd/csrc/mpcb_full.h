@@ -202,7 +202,8 @@ struct FullArgs {
   T h, s;
   Model<T> M;
   const Weights17<T>* W;
-  const T* p; int64_t p_sb;   // parameters [B|1, 25]; nullptr -> W->p
+  const T* p; int64_t p_sb, p_kb;   // parameters [B|1][N|1][25] (instance / stage strides, 0 =
+                                   // broadcast); nullptr -> W->p
   const T* x0; int64_t x0_sb;
   const T* xref; int64_t xref_sb;
   const T* uref; int64_t uref_sb;
@@ -225,7 +226,7 @@ __host__ __device__ constexpr int64_t full17_elems(int N) {
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev = nullptr);
 template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
-                              const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st);
+                              int64_t p_kb, const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st);
 template <class T>
 hipError_t launch_sim_step17(int64_t B, T h, const Model<T>& M, const T* p, int64_t p_sb,
                              const T* x, const T* u, T* xo, hipStream_t st);

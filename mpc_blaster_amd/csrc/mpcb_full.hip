@@ -116,7 +116,9 @@ __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
     return;
   }
   P17<T> P;
-  unpack_p17(a.p ? a.p + b * a.p_sb : a.W->p, P);
+  const T* pb = a.p ? a.p + b * a.p_sb : a.W->p;
+  const int64_t pkb = a.p ? a.p_kb : 0;   // stage-varying parameters (acados set(k, 'p'))
+  unpack_p17(pb, P);
   const T* ur = a.uref + b * a.uref_sb;
   T x[NX17], u[NU17];
 #pragma unroll
@@ -131,6 +133,7 @@ __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
       w.UB[(int64_t)k * NU17 + m] = u[m];
     }
     T xn[NX17];
+    if (pkb && k) unpack_p17(pb + k * pkb, P);
     rk4_17<T, false>(x, nullptr, u, nullptr, a.h, a.M, P, xn, nullptr);
 #pragma unroll
     for (int i = 0; i < NX17; ++i) {
@@ -145,7 +148,7 @@ __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
 // forward VDE).  LIN_WS: into the workspace (+ gaps, iterate mode); else into dense A / Bm.
 template <class T, bool LIN_WS>
 __device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>& M, const T* p,
-                                           int64_t p_sb, const T* xbar, const T* ubar, int64_t b0,
+                                           int64_t p_sb, int64_t p_kb, const T* xbar, const T* ubar, int64_t b0,
                                            T* ws, int mode, T* A, T* Bm, T* xnext) {
   const int lane = threadIdx.x;
   const int j = lane % L17;
@@ -155,7 +158,7 @@ __device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>
   const int k = (int)(idx % N);
   const int64_t b = b0 + c;
   P17<T> P;
-  unpack_p17(p + b * p_sb, P);
+  unpack_p17(p + b * p_sb + k * p_kb, P);
   const T* xk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)k * NX17 : xbar + (b * (N + 1) + k) * NX17;
   const T* uk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)(N + 1) * NX17 + (int64_t)k * NU17
                        : ubar + (b * N + k) * NU17;
@@ -210,7 +213,7 @@ __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
   const int64_t c = idx / N;
   const int k = (int)(idx % N);
   const int64_t b = a.b0 + c;
-  const T* pb = a.p ? a.p + b * a.p_sb : a.W->p;
+  const T* pb = a.p ? a.p + b * a.p_sb + k * a.p_kb : a.W->p;
   Ws17<T> w(a.ws + c * full17_elems(N), N);
   T* ABk = w.AB + (int64_t)k * NZ17 * NX17;
   if (t >= 14) {
@@ -799,9 +802,10 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
 // [A|B] of every shooting interval into dense arrays (debug / parity, mpcb_linearize).
 template <class T>
 __global__ void __launch_bounds__(64) linearize17_kernel(int64_t B, int N, T h, Model<T> M,
-                                                         const T* p, int64_t p_sb, const T* xbar,
-                                                         const T* ubar, T* A, T* Bm, T* xnext) {
-  lin17_body<T, false>(B, N, h, M, p, p_sb, xbar, ubar, 0, nullptr, 0, A, Bm, xnext);
+                                                         const T* p, int64_t p_sb, int64_t p_kb,
+                                                         const T* xbar, const T* ubar, T* A, T* Bm,
+                                                         T* xnext) {
+  lin17_body<T, false>(B, N, h, M, p, p_sb, p_kb, xbar, ubar, 0, nullptr, 0, A, Bm, xnext);
 }
 
 template <class T>
@@ -836,9 +840,10 @@ template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st
 }
 template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
-                              const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st) {
+                              int64_t p_kb, const T* xbar, const T* ubar, T* A, T* Bm, T* xnext,
+                              hipStream_t st) {
   const unsigned grid = (unsigned)((B * N + G17 - 1) / G17);
-  hipLaunchKernelGGL(linearize17_kernel<T>, dim3(grid), dim3(64), 0, st, B, N, h, M, p, p_sb, xbar,
+  hipLaunchKernelGGL(linearize17_kernel<T>, dim3(grid), dim3(64), 0, st, B, N, h, M, p, p_sb, p_kb, xbar,
                      ubar, A, Bm, xnext);
   return hipGetLastError();
 }
@@ -853,10 +858,10 @@ hipError_t launch_sim_step17(int64_t B, T h, const Model<T>& M, const T* p, int6
 template hipError_t launch_full17<double>(const FullArgs<double>&, hipStream_t, hipEvent_t*);
 template hipError_t launch_full17<float>(const FullArgs<float>&, hipStream_t, hipEvent_t*);
 template hipError_t launch_linearize17<double>(int64_t, int, double, const Model<double>&, const double*,
-                                               int64_t, const double*, const double*, double*, double*,
+                                               int64_t, int64_t, const double*, const double*, double*, double*,
                                                double*, hipStream_t);
 template hipError_t launch_linearize17<float>(int64_t, int, float, const Model<float>&, const float*,
-                                              int64_t, const float*, const float*, float*, float*,
+                                              int64_t, int64_t, const float*, const float*, float*, float*,
                                               float*, hipStream_t);
 template hipError_t launch_sim_step17<double>(int64_t, double, const Model<double>&, const double*, int64_t,
                                               const double*, const double*, double*, hipStream_t);

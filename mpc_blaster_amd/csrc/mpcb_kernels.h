@@ -91,6 +91,8 @@ struct SplitArgs {
   T* XU; T* CC; T* GP; T* KR;
   T* AB; T* ABT; T* GH;   // box path: P2 exports the linearisation and the Hessian's input rows
   T* PS;             // box path: value-function snapshots for restarts
+  int32_t* qp_stats; // box path (nullable): per global instance [forward passes, masked backward
+                     // stages] until its active set converged
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

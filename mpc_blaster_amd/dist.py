@@ -83,3 +83,80 @@ def run_sharded(solve_fn: Callable, make_inputs_fn: Callable, global_batch: int,
     if gather:
         return sh, gather_u0(u0, sh, global_batch)
     return sh, u0
+
+
+class StepPipeline:
+    """The timed step of ``bench.py``: solve this rank's batch, then the one collective.
+
+    ``solve(out)`` writes the rank's outputs into ``out`` = (u0 [B, nu], X|None, U|None, status)
+    on the current stream.  Per step the rank then either all-gathers u0 into [world*B, nu]
+    (c2-c4, ``mode='gather'``) or reduces u0 to a per-motor int64 histogram with
+    ``histogram(u0, counts)`` and all-reduces it (c5, ``mode='histogram'``).  With several ranks
+    the collective is issued asynchronously (RCCL runs it on the process group's own stream) and
+    the outputs are double-buffered: step i's collective overlaps step i+1's solve, and an output
+    set is written again only after its collective has been waited on.  The gloo test
+    (tests/test_dist_gloo.py) drives this same class with a CPU solve.
+    """
+
+    def __init__(self, make_outputs: Callable, mode: str, world: int, histogram: Callable | None = None,
+                 nbins: int = 64, group=None):
+        import torch
+        if mode not in ('gather', 'histogram'):
+            raise ValueError(f'mode {mode!r}')
+        if mode == 'histogram' and histogram is None:
+            raise ValueError('histogram mode needs the histogram function')
+        self.mode, self.world, self.group = mode, int(world), group
+        self.histogram = histogram
+        self.nbuf = 2 if self.world > 1 else 1
+        self.outs = [make_outputs() for _ in range(self.nbuf)]
+        u0 = self.outs[0][0]
+        self.gathered = ([torch.empty((self.world * u0.shape[0],) + tuple(u0.shape[1:]), dtype=u0.dtype,
+                                      device=u0.device) for _ in range(self.nbuf)]
+                         if (mode == 'gather' and self.world > 1) else None)
+        self.counts = [torch.zeros((u0.shape[1], nbins), dtype=torch.int64, device=u0.device)
+                       for _ in range(self.nbuf)] if mode == 'histogram' else None
+        self.pending = [None] * self.nbuf
+        self.it = 0
+        self.last = 0
+
+    def step(self, solve: Callable, before: Callable | None = None, after: Callable | None = None):
+        """One step; ``before`` / ``after`` run around the solve (e.g. HIP event records)."""
+        import torch.distributed as dist
+        i = self.it % self.nbuf
+        self.it += 1
+        self.last = i
+        if self.pending[i] is not None:
+            self.pending[i].wait()
+            self.pending[i] = None
+        o = self.outs[i]
+        if before is not None:
+            before()
+        solve(o)
+        if after is not None:
+            after()
+        if self.mode == 'histogram':
+            self.counts[i].zero_()
+            self.histogram(o[0], self.counts[i])
+            if self.world > 1:
+                self.pending[i] = dist.all_reduce(self.counts[i], op=dist.ReduceOp.SUM,
+                                                  group=self.group, async_op=True)
+        elif self.world > 1:
+            self.pending[i] = dist.all_gather_into_tensor(self.gathered[i], o[0], group=self.group,
+                                                          async_op=True)
+
+    def drain(self):
+        for i in range(self.nbuf):
+            if self.pending[i] is not None:
+                self.pending[i].wait()
+                self.pending[i] = None
+
+    def result(self, i: int | None = None):
+        """After ``drain()``: the gathered u0 [world*B, nu] (gather; this rank's u0 on one rank)
+        or the all-reduced histogram [nu, nbins] of the output set ``i`` (default: the last)."""
+        i = self.last if i is None else i
+        if self.mode == 'histogram':
+            return self.counts[i]
+        return self.gathered[i] if self.gathered is not None else self.outs[i][0]
+
+    def bad_status(self) -> int:
+        return int(sum(int((o[3] != 0).sum()) for o in self.outs))

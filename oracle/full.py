@@ -136,20 +136,21 @@ def rk4_sens17(x, u, p25, h, P: Params):
 
 def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=None, ubar=None):
     """One SQP_RTI step of the 17/6 OCP for a batch: x0 (B,17), xref (B|1,N+1,17), uref (B|1,N,6),
-    p25 (B|1,25) (acados ``set(k, 'p', p)``, the same vector on every stage)."""
+    p25 (B|1,25) the same vector on every stage, or (B|1,N,25) stage by stage (acados
+    ``set(k, 'p', p)``, simulation_blaster.py:65-69: stage k's vector enters interval k)."""
     x0 = np.asarray(x0, dtype=np.float64)
     Bsz, N = x0.shape[0], spec.N
     xref = np.broadcast_to(np.asarray(xref, dtype=np.float64), (Bsz, N + 1, NX17))
     uref = np.broadcast_to(np.asarray(uref, dtype=np.float64), (Bsz, N, NU17))
-    p25 = np.broadcast_to(default_p25() if p25 is None else np.asarray(p25, dtype=np.float64),
-                          (Bsz, NP17))
+    p25 = default_p25() if p25 is None else np.asarray(p25, dtype=np.float64)
+    pk = np.broadcast_to(p25[..., :N, :] if p25.ndim == 3 else p25[..., None, :], (Bsz, N, NP17))
     P = spec.params
     if mode == 'rollout':
         ubar = uref.copy()
         xbar = np.empty((Bsz, N + 1, NX17))
         xbar[:, 0] = x0
         for k in range(N):
-            xbar[:, k + 1] = rk4_step17(xbar[:, k], ubar[:, k], p25, spec.dt, P)
+            xbar[:, k + 1] = rk4_step17(xbar[:, k], ubar[:, k], pk[:, k], spec.dt, P)
     else:
         xbar = np.asarray(xbar, dtype=np.float64)
         ubar = np.asarray(ubar, dtype=np.float64)
@@ -157,7 +158,7 @@ def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=N
     Bm = np.empty((Bsz, N, NX17, NU17))
     gap = np.empty((Bsz, N, NX17))
     for k in range(N):
-        xn, A[:, k], Bm[:, k] = rk4_sens17(xbar[:, k], ubar[:, k], p25, spec.dt, P)
+        xn, A[:, k], Bm[:, k] = rk4_sens17(xbar[:, k], ubar[:, k], pk[:, k], spec.dt, P)
         gap[:, k] = xn - xbar[:, k + 1]
     if mode == 'rollout':
         gap[:] = 0.0   # the rollout is gap-free by construction

@@ -354,3 +354,91 @@ def test_solve17_fp32_input_box_close_to_fp64_oracle():
     with pytest.raises(_lib.MpcbError, match='f64'):
         BatchedMPC(MPCConfig.full(N=N, dtype='f32', lbu=LBU17, ubu=UBU17, lbx=-np.ones(17), ubx=np.ones(17)),
                    max_batch=B)
+
+
+def _reference_blaster_model(**kw):
+    """blasterModel(...) with simulation_blaster.py:12-30's exact arguments (N = 60, Tf = 2,
+    blastThruster = 2.2 * 9.81, statesBound, controlBound) on the full model."""
+    from mpc_blaster_amd.compat.blastermodel import blasterModel
+    J = np.eye(3)
+    J[0, 0], J[1, 1], J[2, 2] = 0.50781, 0.47314, 0.72975
+    Q = np.zeros((17, 17))
+    np.fill_diagonal(Q, [1e3, 1e3, 1e3, 1e3, 1e3, 1e3, 0.5e1, 0.5e1, 0.5e1, 1e1, 1e1, 1e1, 1e-2, 1e-2,
+                         1e3, 1e3, 1e3])
+    R = np.zeros((6, 6))
+    np.fill_diagonal(R, [5e-2, 5e-2, 5e-2, 5e-2, 1e-5, 1e-5])
+    return blasterModel(9.0, J, 0.3434, 0.3475, 60, 2.0, 0.03, Q, R, 10 * Q, 2.2 * 9.81,
+                        np.stack([SB_LO, SB_HI]), np.stack([LBU17, UBU17]), full_model=True, **kw)
+
+
+def test_facade_reference_arguments_default_then_stage_varying_p():
+    """The reference's own constructor arguments: the first solve runs before any set('p') on
+    acados' default parameter vector (T_blast = 2.2*9.81 whatever blastThruster is,
+    blastermodel.py:280-282), the second with a different p on every stage (set(k, 'p') per
+    stage, simulation_blaster.py:65-69) — both against the oracle's SQP_RTI iterate."""
+    b = _reference_blaster_model()
+    b.generateModel()
+    assert b._cfg.t_blast == pytest.approx(21.582, rel=1e-15)
+    integrator, ocp = b.generateController()
+    N = 60
+    spec = FullSpec(N=N, lbu=LBU17, ubu=UBU17, lbx=SB_LO, ubx=SB_HI)
+    x = np.zeros(17)                                      # simulation_blaster.py:46
+    yref = np.zeros(23)
+    yref[2], yref[14] = 3.5, 0.2                          # simulation_blaster.py:48
+    xr = np.broadcast_to(yref[:17], (1, N + 1, 17))
+    ur = np.zeros((1, N, 6))
+    rng = np.random.default_rng(11)
+    pk = np.tile(default_p25(), (N, 1))
+    pk[:, :24] = rng.uniform(-0.3, 0.3, (N, 24))
+    xbar, ubar = np.zeros((1, N + 1, 17)), np.zeros((1, N, 6))
+    for it in range(2):
+        if it == 1:
+            for k in range(N):
+                ocp.set(k, 'p', pk[k])
+        ocp.set(0, 'lbx', x)
+        ocp.set(0, 'ubx', x)
+        for k in range(N + 1):
+            ocp.cost_set(k, 'yref', yref if k < N else yref[:17])
+        assert ocp.solve() == 0
+        o = mpc_solve17(x[None], xr, ur, spec, None if it == 0 else pk[None], mode='iterate',
+                        xbar=xbar, ubar=ubar)
+        xbar, ubar = o['X'], o['U']
+        assert o['status'][0] == 0
+        eu = relerr(ocp.get(0, 'u')[None], o['u0']).max()
+        ex = relerr(np.stack([ocp.get(k, 'x') for k in range(N + 1)])[None], o['X']).max()
+        print(f'solve {it}: u0 err {eu:.2e}, X err {ex:.2e}')
+        assert eu < 1e-7 and ex < 1e-7
+
+
+def test_set_params_rows_checked_against_batch():
+    """A solve / linearize / sim_step over more instances than the parameter rows is refused
+    (no out-of-bounds device read); broadcast rows (one vector) serve any batch."""
+    from mpc_blaster_amd._lib import MpcbError
+    N, B = 6, 5
+    x0, xref, uref, p = _inputs(B, N, 3)
+    m = _mpc(N, max_batch=B)
+    m.set_params(p[:2])
+    with pytest.raises(MpcbError, match='parameter rows'):
+        m.solve(x0, xref, uref)
+    with pytest.raises(MpcbError, match='parameter rows'):
+        m.sim_step(x0, uref[:, 0])
+    m.set_params(p[:1])
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N), p[:1])
+    assert relerr(m.get_control().cpu().numpy(), o['u0']).max() < 1e-9
+
+
+def test_set_t_blast_updates_default_parameter_in_place():
+    N, B = 8, 4
+    x0, xref, uref, _ = _inputs(B, N, 5)
+    m = _mpc(N, max_batch=B)
+    h = m._h.value
+    m.set_t_blast(15.0)
+    assert m._h.value == h
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    p = default_p25()
+    p[24] = 15.0
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N), p[None])
+    assert relerr(m.get_control().cpu().numpy(), o['u0']).max() < 1e-9

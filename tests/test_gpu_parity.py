@@ -62,7 +62,7 @@ def test_library_is_the_native_hip_build():
     from mpc_blaster_amd import _lib
     lib = _lib.load()
     assert os.path.basename(lib._name) == 'libmpcblaster.so'
-    assert lib.mpcb_abi_version() == 3
+    assert lib.mpcb_abi_version() == 4
 
 
 def test_linearize_matches_oracle_fp64():
@@ -231,6 +231,72 @@ def test_full_size_c3_properties():
     assert relerr(X[idx].cpu().numpy(), o['X']).max() < 5e-5
 
 
+@pytest.mark.parametrize('want_traj', [False, True])
+@pytest.mark.parametrize('path', [None, 'fused'])
+def test_c5_matches_oracle_fp32(want_traj, path):
+    """BASELINE c5 (configs[4]): N = 40, fp32, hover reference, per-instance wind force; the
+    u0-only P2 (want_traj=False: the Riccati kernel writes u0, no forward pass) and the full
+    trajectory, against the fp64 oracle on the fp32-rounded inputs."""
+    B, N = 203, 40
+    inp = make_inputs('c5', ids=np.arange(B, dtype=np.uint64), N=N)
+    m = _mpc(N, 'f32', max_batch=B, path=path)
+    m.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=want_traj)
+    torch.cuda.synchronize()
+    cast = lambda a: a.astype(np.float32).astype(np.float64)
+    o = mpc_solve(cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), _spec(N), wind=cast(inp['wind']))
+    e_u = relerr(m.get_control().cpu().numpy(), o['u0'])
+    msg = f'c5 N=40 f32 path={path} traj={want_traj}: u0 {e_u.max():.2e}'
+    assert (m.get_status().cpu().numpy() == 0).all()
+    assert e_u.max() < 5e-5
+    if want_traj:
+        e_x = relerr(m.get_state_trajectory().cpu().numpy(), o['X'])
+        e_U = relerr(m.get_input_trajectory().cpu().numpy(), o['U'])
+        msg += f' X {e_x.max():.2e} U {e_U.max():.2e}'
+        assert e_x.max() < 5e-5 and e_U.max() < 5e-5
+    print(msg)
+
+
+def _host_histogram(u0, lo=0.0, hi=65.0, nbins=64):
+    """The kernel's binning restated: bin = floor((double(u) - lo) * nbins / (hi - lo)), clipped."""
+    v = np.asarray(u0, dtype=np.float64)
+    b = np.floor((v - lo) * (nbins / (hi - lo)))
+    b = np.where(np.isnan(v), nbins - 1, np.clip(b, 0, nbins - 1)).astype(np.int64)
+    return np.stack([np.bincount(b[:, m], minlength=nbins) for m in range(v.shape[1])])
+
+
+def test_full_size_c5_histogram_properties():
+    """BASELINE c5 per-GPU shard (131072 of 1048576 on 8 GPUs, N = 40, fp32, wind): every status
+    0, u0 finite; the 64-bin per-motor histogram sums to B per motor and equals the host binning
+    of the device u0 bit for bit; the u0-only solve equals the trajectory solve; sampled parity."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    B, N = 131072, 40
+    m = BatchedMPC(MPCConfig(N=N, dtype='f32'), max_batch=B)
+    d = m.gen_inputs(B, seed=1005, id_offset=3 * B, ref='hover', wind=True)   # rank 3's ids
+    u0 = m.solve(d['x0'], d['xref'], d['uref'], wind=d['wind'], want_traj=False).clone()
+    st = m.get_status().clone()
+    counts = m.histogram(u0, 0.0, 65.0, 64)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.isfinite(u0).all()
+    c = counts.cpu().numpy()
+    assert (c.sum(axis=1) == B).all()
+    assert np.array_equal(c, _host_histogram(u0.cpu().numpy()))
+    # the u0-only Riccati kernel and the full path agree
+    u_full = m.solve(d['x0'], d['xref'], d['uref'], wind=d['wind'], want_traj=True)
+    torch.cuda.synchronize()
+    assert torch.equal(u_full, u0)
+    # the device's synthetic inputs are the oracle's (fp32-rounded) and sampled instances match it
+    idx = np.arange(0, B, 5003)
+    o_in = make_inputs('c5', ids=np.uint64(3 * B) + idx.astype(np.uint64), N=N)
+    cast = lambda a: a.astype(np.float32).astype(np.float64)
+    assert np.array_equal(d['x0'][idx].double().cpu().numpy(), cast(o_in['x0']))
+    assert np.array_equal(d['wind'][idx].double().cpu().numpy(), cast(o_in['wind']))
+    o = mpc_solve(cast(o_in['x0']), cast(o_in['xref']), cast(o_in['uref']), _spec(N), wind=cast(o_in['wind']))
+    e = relerr(u0[idx].cpu().numpy(), o['u0'])
+    print(f'c5 full size: sampled u0 err {e.max():.2e}; hist bins occupied {int((c > 0).sum())}')
+    assert e.max() < 5e-5
+
+
 def test_full_size_c4_box_properties():
     """BASELINE c4 per-GPU shard (65536, N=30, fp32, thrust box [0, 65]): every instance reaches
     its KKT point (no MAXITER), bounds hold, sampled oracle parity, and the single-kernel
@@ -285,9 +351,13 @@ def test_closed_loop_matches_oracle_fp64():
     assert (st.cpu().numpy() == 0).all()
 
 
-def test_acados_facade_runs_reference_loop():
+@pytest.mark.parametrize('t_blast', ['default', 'zero'])
+def test_acados_facade_runs_reference_loop(t_blast):
     """simulation_blaster.py-style loop through the compat facade (12/4 slice of the reference
-    parameter set, reference-length 17/23 vectors sliced)."""
+    parameter set, reference-length 17/23 vectors sliced).  ``default``: no set('p'), so the
+    slice flies with acados' default T_blast = 2.2*9.81 (blastermodel.py:280-282); ``zero``:
+    set(k, 'p') / integrator.set('p') with p[24] = 0 on every stage (a quad without the blaster),
+    applied on the same device handle."""
     from mpc_blaster_amd.compat.blastermodel import blasterModel
     J = np.diag([0.50781, 0.47314, 0.72975])
     Q = np.zeros((17, 17))
@@ -304,9 +374,16 @@ def test_acados_facade_runs_reference_loop():
     yref = np.zeros(23)
     yref[2] = 3.5
     lbu, ubu = np.zeros(4), np.full(4, 65.0)
-    spec = OcpSpec(N=N, lbu=lbu, ubu=ubu)
+    tb = 2.2 * 9.81 if t_blast == 'default' else 0.0
+    P = Params(t_blast=tb)
+    spec = OcpSpec(N=N, lbu=lbu, ubu=ubu, params=P)
     xbar, ubar = np.zeros((1, N + 1, 12)), np.zeros((1, N, 4))
     xs = x[:12].copy()
+    handle = ocp_solver.mpc._h.value
+    if t_blast == 'zero':
+        for k in range(N):
+            ocp_solver.set(k, 'p', np.zeros(25))
+        integrator.set('p', np.zeros(25))
     for i in range(5):
         ocp_solver.set(0, 'lbx', x)
         ocp_solver.set(0, 'ubx', x)
@@ -325,5 +402,6 @@ def test_acados_facade_runs_reference_loop():
         assert integrator.solve() == 0
         x = np.r_[integrator.get('x'), np.zeros(5)]
         from oracle.rk4 import rk4_step
-        xs = rk4_step(xs[None], o['u0'], 1.0 / 30.0, Params())[0]
+        xs = rk4_step(xs[None], o['u0'], 1.0 / 30.0, P)[0]
         assert np.abs(x[:12] - xs).max() < 1e-9
+    assert ocp_solver.mpc._h.value == handle     # T_blast changed in place, not by re-creation
