@@ -26,6 +26,14 @@
 
 namespace mpcb {
 
+#ifdef MPCB_STAMPS
+// Diagnostic build only: per-region cycles of the 16-lane forward pass (PASS_FWD) of workgroup 0
+__device__ unsigned long long g_bstamps[8];
+#define BSTAMP(i) if constexpr (MODE == PASS_FWD) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); bst_acc[i] += t_ - bst_prev; bst_prev = t_; }
+#else
+#define BSTAMP(i)
+#endif
+
 #ifndef MPCB_BOX_WAVES
 #define MPCB_BOX_WAVES 2
 #endif
@@ -341,8 +349,12 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         fa[sl][NZ] = iterate ? soa(a.GP, k, GP_REC, nb, c)[jx * SS] : T(0);
       }
     };
+#ifdef MPCB_STAMPS
+    unsigned long long bst_prev = __builtin_amdgcn_s_memtime(), bst_acc[8] = {};
+#endif
     auto stage = [&](int k, auto sl_tag) {
       constexpr int sl = decltype(sl_tag)::value;
+      BSTAMP(0);
       T ra[NZ + 1], rb[NX + 1];
 #pragma unroll
       for (int i = 0; i <= NZ; ++i) ra[i] = fa[sl][i];
@@ -350,6 +362,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       for (int i = 0; i <= NX; ++i) rb[i] = fb[sl][i];
       const T yb = fyb[sl];
       if (k + DEPTH < N) fload(k + DEPTH, sl_tag);
+      BSTAMP(1);
       L.v[j] = dxj;   // input lanes overwrite their slot with du below
       wave_lds_sync();
       const bool lo = (sel<NU>(low, ju) >> k) & 1ull, hi = (sel<NU>(up, ju) >> k) & 1ull;
@@ -363,11 +376,13 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         dxj = du;
       }
       wave_lds_sync();
+      BSTAMP(2);
       if (j >= NX) L.v[j] = dxj;
       wave_lds_sync();
       T z[NZ];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) z[i] = L.v[i];
+      BSTAMP(3);
       if (j >= NX) {
         const T du = dxj;
         const T uk = yb + du;
@@ -399,6 +414,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         dxj = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       }
       wave_lds_sync();
+      BSTAMP(4);
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
@@ -409,6 +425,11 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       if (DEPTH == 2 && k + 1 < N) stage(k + 1, S1());
     }
     if (write && a.X && j < NX) a.X[(b * (N + 1) + N) * NX + jx] = soa(a.XU, N, XU_REC, nb, c)[jx * SS] + dxj;
+#ifdef MPCB_STAMPS
+    if constexpr (MODE == PASS_FWD)
+      if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int i_ = 0; i_ < 8; ++i_) g_bstamps[i_] = bst_acc[i_];
+#endif
 
     if constexpr (!BOX) break;
     // ------------------------------------------------ active-set update (Kim-Park)
@@ -552,3 +573,9 @@ template hipError_t launch_fwd16<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_fwd16<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb
+
+#ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_stamps_box(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_bstamps), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -30,8 +30,23 @@
 #define MPCB_P1_ALLW 1
 #endif
 
+// P1: broadcast u_ref rows staged in LDS (up to MPCB_P1_UMAX stages)
+#ifndef MPCB_P1_ULDS
+#define MPCB_P1_ULDS 1
+#endif
+#ifndef MPCB_P1_UMAX
+#define MPCB_P1_UMAX 64
+#endif
+
 #ifndef MPCB_P2_WAVES
 #define MPCB_P2_WAVES
+#endif
+
+#ifndef MPCB_P2_SWT
+#define MPCB_P2_SWT 1
+#endif
+#ifndef MPCB_P2_CPAD
+#define MPCB_P2_CPAD 16
 #endif
 
 #ifndef MPCB_P2_WAVES_F32
@@ -46,7 +61,7 @@ namespace mpcb {
 __device__ unsigned long long g_stamps[16];
 #define STAMP_INIT() unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
 #define STAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_prev; st_prev = t_; }
-#define STAMP_DONE() if (blockIdx.x == 0 && threadIdx.x == 0) for (int i_ = 0; i_ < 16; ++i_) g_stamps[i_] = st_acc[i_];
+#define STAMP_DONE() if (blockIdx.x == 0 && threadIdx.x == 0) for (int i_ = 0; i_ < 16; ++i_) if (st_acc[i_]) g_stamps[i_] = st_acc[i_];
 #else
 #define STAMP_INIT()
 #define STAMP(i)
@@ -264,9 +279,25 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
   const T* ur = a.uref + b * a.uref_sb;
   T x[NX], u[NU];
   load_vec<NX>(iterate ? xbp : a.x0 + b * a.x0_sb, x);
+  // a broadcast input reference (uref_sb == 0: c2, c4, c5) is staged in LDS once, so that the
+  // chain's only vector-memory operations are the flush stores (no per-stage load waiting
+  // behind them on vmcnt)
+  __shared__ T lds_u[MPCB_P1_UMAX * NU];
+  const bool ubc = MPCB_P1_ULDS && !iterate && a.uref_sb == 0 && N <= MPCB_P1_UMAX;
+  if (ubc) {
+    for (int e = lane; e < N * NU; e += WAVE) lds_u[e] = a.uref[e];
+    wave_lds_sync();
+  }
+  STAMP_INIT();
   for (int k = 0; k < N; ++k) {
+    STAMP(13);
     if (iterate) load_vec<NX>(xbp + (int64_t)k * NX, x);
-    load_vec<NU>(iterate ? ubp + (int64_t)k * NU : ur + (int64_t)k * NU, u);
+    if (ubc) {
+#pragma unroll
+      for (int m = 0; m < NU; ++m) u[m] = lds_u[k * NU + m];
+    } else {
+      load_vec<NU>(iterate ? ubp + (int64_t)k * NU : ur + (int64_t)k * NU, u);
+    }
     if (lead) {
 #pragma unroll
       for (int i = 0; i < NX; ++i) xus.put(ci, i, x[i]);
@@ -280,6 +311,7 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
         for (int i = 0; i < LIN_N; ++i) ccs.put(ci, stage * LIN_N + i, cv[i]);
       }
     }, trig);
+    STAMP(14);
     if (iterate) {
       const T* nx = xbp + (int64_t)(k + 1) * NX;
       if (lead) {
@@ -295,7 +327,9 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
     ccs.flush(lane, soa(a.CC, k, CCS_REC, nb, c0), nqv);
     if (iterate) gps.flush(lane, soa(a.GP, k, GP_REC, nb, c0), nqv);
     wave_lds_sync();
+    STAMP(15);
   }
+  STAMP_DONE();
   if (iterate) load_vec<NX>(xbp + (int64_t)N * NX, x);
   if (lead) {
 #pragma unroll
@@ -363,7 +397,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   // component of ybar and yref, one gap value per lane) and committed to a double-buffered LDS
   // copy, so the tangent integrates from LDS and no global-load latency sits on the chain.
   // (every lane loads and commits through one address select: no divergent branch)
-  __shared__ T Cst[2][GROUPS][CCS_REC + NZ];
+  // group stride padded so that two groups' broadcast reads of the same scalar fall on different
+  // banks (96 elements put them on one bank: a 2-way conflict on every tangent read)
+  __shared__ T Cst[2][GROUPS][CCS_REC + NZ + MPCB_P2_CPAD];
   T pc[5], pyb, pyr, pgp = T(0);
   auto prefetch = [&](int k) {
     const T* cc = soa(a.CC, k, CCS_REC, nb, c);
@@ -472,7 +508,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(3);
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
-      const T w = SW[j * NZ + i];
+      // SW is symmetric: lane j reads column j so the 16 lanes hit 16 consecutive entries (row j
+      // put every second lane on the same bank: an 8-way conflict on each of these reads)
+      const T w = MPCB_P2_SWT ? SW[i * NZ + j] : SW[j * NZ + i];
       G[i] += w;
       hj += w * L.v[i];
     }

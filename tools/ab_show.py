@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Summarise gpurun_out/<dir>/bench_*.log lines from tools/ab_p2.sh."""
-import glob, json, os, sys
+"""Summarise an A/B directory written by tools/ab_tmp.sh: value and phase ms per log."""
+import glob
+import json
+import os
+import sys
+
 d = sys.argv[1]
-for f in sorted(glob.glob(os.path.join('gpurun_out', d, 'bench_*.log'))):
+for f in sorted(glob.glob(os.path.join(d, '*.log'))):
     try:
-        r = json.loads(open(f).read().strip().splitlines()[-1])
-    except Exception as e:
-        print(f, 'unparsable', e); continue
-    ro = r['roofline']; sec = r.get('secondary') or {}
-    print(f"{os.path.basename(f):24s} {r['value']:.4g} frac {ro['frac']:.3f} phases "
-          + ' '.join(f"{k}={v*1e3:.1f}us" for k, v in ro['phase_ms'].items())
-          + (f" | c3 {sec['value']:.4g}" if sec else ''))
+        line = json.loads(open(f).read().strip().splitlines()[-1])
+    except Exception:
+        continue
+    r = line['roofline']
+    ph = ' '.join(f'{k}={v * 1000:.1f}' for k, v in r['phase_ms'].items())
+    print(f'{os.path.basename(f):24s} {line["value"] / 1e6:8.2f}M/s  {line["ms_per_step"] * 1000:8.1f}us  {ph}  frac={r["frac"]:.3f}')

@@ -32,3 +32,18 @@ print(f'{w}: cycles per stage (s_memtime units, wave 0):')
 for n, x in zip(names, v):
     print(f'   {n:24s} {x:9.0f}')
 print(f'   {"total":24s} {v.sum():9.0f}')
+v1 = np.array(out[13:16], dtype=np.float64) / N
+print(f'{w}: P1 (nominal_quad) cycles per stage (wave 0):')
+for n, x in zip(['u load + xu puts', 'rk4_nom (4 f + capture puts)', 'flush + syncs'], v1):
+    print(f'   {n:32s} {x:9.0f}')
+print(f'   {"total":32s} {v1.sum():9.0f}')
+
+if hasattr(lib, 'mpcb_debug_stamps_box'):
+    ob = (ctypes.c_ulonglong * 8)()
+    lib.mpcb_debug_stamps_box.argtypes = [ctypes.c_void_p]
+    if lib.mpcb_debug_stamps_box(ob) == 0:
+        vb = np.array(ob[:5], dtype=np.float64) / N
+        print(f'{w}: P3 (16-lane forward) cycles per stage (wave 0):')
+        for n, x in zip(['stage start -> regs (+prefetch wait)', 'fload issue', 'du dot', 'publish du, read z', 'outputs + state dot'], vb):
+            print(f'   {n:36s} {x:9.0f}')
+        print(f'   {"total":36s} {vb.sum():9.0f}')
