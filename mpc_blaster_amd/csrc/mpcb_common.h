@@ -41,22 +41,45 @@ template <class T> __device__ __forceinline__ T opq(T x) {
   return x;
 }
 
-// a[j] (0 <= j < 16, n <= 16) for a register array, as a bit-tree of selects.  Without the
-// opaque copies InstCombine folds select(load a[i], load a[k]) into a load from a selected
-// address, which turns the register array into a dynamically indexed scratch array.
-template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
-  T l0[8], l1[4], l2[2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const T lo = opq(a[(2 * i < n) ? 2 * i : n - 1]);
-    const T hi = opq(a[(2 * i + 1 < n) ? 2 * i + 1 : n - 1]);
-    l0[i] = (j & 1) ? hi : lo;
+// Per-lane m ? a : b for a lane mask m held in SGPRs (m = ballot of the condition): one
+// v_cndmask_b32 per dword.  A C++ ?: on values the compiler cannot speculate (the results of
+// asm statements) becomes exec-masked branches; on array elements InstCombine may fold it into a
+// load from a selected address (a dynamically indexed scratch array).  This is neither.
+__device__ __forceinline__ unsigned cnd32(uint64_t m, unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
+}
+template <class T> __device__ __forceinline__ T csel(uint64_t m, T a, T b) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "csel: 32- or 64-bit values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, cnd32(m, __builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b)));
+  } else {
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+    const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+    const unsigned lo = cnd32(m, (unsigned)ua, (unsigned)ub);
+    const unsigned hi = cnd32(m, (unsigned)(ua >> 32), (unsigned)(ub >> 32));
+    return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
   }
+}
+__device__ __forceinline__ uint64_t lane_mask(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// a[j] (0 <= j < n <= 16) for a register array: a bit-tree of csel on the bits of j.
+template <int n, int bit, class T> __device__ __forceinline__ T sel_level(const T* a, int j) {
+  if constexpr (n == 1) {
+    return a[0];
+  } else {
+    constexpr int w = (n + 1) / 2;
+    const uint64_t m = lane_mask((j >> bit) & 1);
+    T l[w];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) l1[i] = (j & 2) ? opq(l0[2 * i + 1]) : opq(l0[2 * i]);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) l2[i] = (j & 4) ? opq(l1[2 * i + 1]) : opq(l1[2 * i]);
-  return (j & 8) ? opq(l2[1]) : opq(l2[0]);
+    for (int i = 0; i < w; ++i) l[i] = csel(m, a[(2 * i + 1 < n) ? 2 * i + 1 : n - 1], a[2 * i]);
+    return sel_level<w, bit + 1>(l, j);
+  }
+}
+template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
+  static_assert(n >= 1 && n <= 16, "sel: 1..16 elements");
+  return sel_level<n, 0>(a, j);
 }
 
 // 1 / sqrt(x): fp32 sqrt + IEEE reciprocal; fp64 from the hardware estimate v_rsq_f64 refined

@@ -49,6 +49,10 @@
 #define MPCB_P2_CPAD 16
 #endif
 
+#ifndef MPCB_P2_PCSEL
+#define MPCB_P2_PCSEL 0
+#endif
+
 #ifndef MPCB_P2_WAVES_F32
 #define MPCB_P2_WAVES_F32 2
 #endif
@@ -588,8 +592,19 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     if (k > 0) commit(buf ^ 1);
     wave_lds_sync();
     STAMP(8);
+#if MPCB_P2_PCSEL
+    {   // unconditional LDS reads + lane-mask selects (no exec-masked branch per entry)
+      const uint64_t st_lane = lane_mask(j < NX);
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        const T o = L.X[i * NX + jx];
+        Pc[i] = csel(st_lane, csel(lane_mask(i <= j), Pn[i], o), T(0));
+      }
+    }
+#else
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
+#endif
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // the LDS fp64 products read P from LDS
       if (j < NX) {
 #pragma unroll
