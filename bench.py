@@ -287,6 +287,7 @@ def main():
     ap.add_argument('--batch', type=int, default=None, help='override the per-GPU batch')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-secondary', action='store_true')
+    ap.add_argument('--no-latency', action='store_true', help='skip the B=1 per-step latency block')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     ap.add_argument('--max-as-iter', type=int, default=200, help='active-set cap (box workload)')
     args = ap.parse_args()
@@ -347,6 +348,9 @@ def main():
         }
         if sec is not None:
             line['secondary'] = sec
+        if world == 1 and args.workload == 'c2' and not args.no_latency:
+            from mpc_blaster_amd.latency import measure_b1
+            line['latency_b1'] = measure_b1(device=dev)
         if not args.no_cpu_baseline and world == 1:
             line['cpu_baseline'] = cpu_baseline(w, args.cpu_budget)
         print(json.dumps(line), flush=True)

@@ -207,6 +207,16 @@ int mpcb_poc_jacobians(int64_t B, const double* pose, double stream_velocity, co
  */
 int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* hip_stream);
 
+/*
+ * Quaternion helpers of utils/MathUtils.py (q = [w, x, y, z], MathUtils.py:9) for B pairs, fp64,
+ * device arrays: prod[b] = q1[b] (x) q2[b] (quatMultiplication, :5-23), inv[b] = conj(q1[b])
+ * (unitQuatInversion, :25-39), rot[b] = R(q1[b]) row-major 3x3 (quat2Rot, :41-54).  Any output
+ * may be NULL; q2 may be NULL when prod is.  The reference evaluates them on CasADi SX and never
+ * on the MPC path (imported at blastermodel.py:4).
+ */
+int mpcb_quat_ops(int64_t B, const double* q1, const double* q2, double* prod, double* inv,
+                  double* rot, void* hip_stream);
+
 /* Histogram of u0 per input channel over [lo, hi) into counts[nu][nbins] (int64, accumulated). */
 int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double lo, double hi, int nbins,
                    int64_t* counts, void* hip_stream);

@@ -20,7 +20,8 @@ STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram', 'mpcb_set_timing',
-           'mpcb_last_timing', 'mpcb_set_params', 'mpcb_set_t_blast', 'mpcb_qp_stats', 'mpcb_poc_jacobians')
+           'mpcb_last_timing', 'mpcb_set_params', 'mpcb_set_t_blast', 'mpcb_qp_stats', 'mpcb_poc_jacobians',
+           'mpcb_quat_ops')
 
 
 class MpcbConfig(ctypes.Structure):
@@ -84,6 +85,7 @@ def load(path: str | None = None):
     lib.mpcb_qp_stats.argtypes = [vp, i64, vp, vp]
     lib.mpcb_poc_jacobians.argtypes = [i64, vp, dbl, ctypes.POINTER(dbl), i32, dbl, vp, vp, vp, vp, vp,
                                        vp, vp]
+    lib.mpcb_quat_ops.argtypes = [i64, vp, vp, vp, vp, vp, vp]
     for name in EXPORTS:
         if name not in ('mpcb_last_error', 'mpcb_workspace_bytes'):
             getattr(lib, name).restype = i32

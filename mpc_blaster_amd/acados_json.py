@@ -8,7 +8,9 @@ parts this build implements onto ``MPCConfig``:
   rigid-body slice of the BASELINE configs out of a 17/6 description);
 * LINEAR_LS cost with selector ``Vx``/``Vu`` (blastermodel.py:228-257): Q = W[:nx,:nx],
   R = W[nx:,nx:], Q_N = W_e; stage scaling = ``time_steps`` (acados' convention, uniform dt);
-* input box ``idxbu``/``lbu``/``ubu`` (blastermodel.py:259-264), on both models;
+* input box ``idxbu``/``lbu``/``ubu`` (blastermodel.py:259-264), on both models (every input
+  boxed, as the reference sets it; a partial idxbu raises);
+* ``qp_solver_iter_max`` (500 in the reference JSON) as the QP iteration cap;
 * ``parameter_values`` (the default p, T_blast at p[24]);
 * ERK, 4 stages, 1 step, Gauss-Newton SQP_RTI with a full step (the only integrator / NLP
   configuration the device implements; anything else raises).
@@ -86,8 +88,13 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
     lbu = ubu = None
     idxbu = list(np.atleast_1d(con.get('idxbu', [])).astype(int))
     if idxbu:
-        lbu = np.full(nu, -1e20)
-        ubu = np.full(nu, 1e20)
+        # the device's input box covers every input (the reference's idxbu = range(nu),
+        # blastermodel.py:261): a partial box would need +-1e20 rows that the interior point
+        # would treat as real constraints (a 1e20 slack dominates its duality measure)
+        if sorted(idxbu) != list(range(nu)):
+            raise ValueError(f'idxbu {idxbu}: the device implements a box on every input (range({nu}))')
+        lbu = np.empty(nu)
+        ubu = np.empty(nu)
         lbu[idxbu] = np.asarray(con['lbu'], dtype=np.float64)
         ubu[idxbu] = np.asarray(con['ubu'], dtype=np.float64)
     p = np.asarray(d.get('parameter_values', np.zeros(int(dims.get('np', 0)))), dtype=np.float64)
@@ -115,8 +122,11 @@ def load_acados_ocp_json(src, slice_12_4: bool = False, dtype: str = 'f64', **ph
         dropped.append('alpha / POC states and swivel inputs (12/4 slice)')
     phys = dict(mass=9.0, J=np.diag([0.50781, 0.47314, 0.72975]), lx=0.3434, ly=0.3475, c=0.03)
     phys.update(physical)
+    # HPIPM's iteration cap (JSON solver_options.qp_solver_iter_max, blastermodel.py:279) caps the
+    # device's active-set / interior-point iterations
+    max_it = int(so.get('qp_solver_iter_max', 200))
     cfg = MPCConfig(N=N, dt=dt, dtype=dtype, Q=Q, R=R, QN=We, cost_scale=dt, lbu=lbu, ubu=ubu,
-                    lbx=lbx, ubx=ubx, t_blast=t_blast, nx=nx, nu=nu, **phys)
+                    lbx=lbx, ubx=ubx, t_blast=t_blast, nx=nx, nu=nu, max_as_iter=max_it, **phys)
     for what in dropped:
         warnings.warn(f'acados JSON: {what} not applied by the device path', stacklevel=2)
     info = dict(yref=np.asarray(cost.get('yref', np.zeros(ny)), dtype=np.float64),

@@ -210,6 +210,50 @@ hipError_t launch_histogram(int64_t B, int nu, const T* u0, double lo, double hi
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------ quaternion helpers
+// utils/MathUtils.py: quatMultiplication (:5-23), unitQuatInversion (:25-39), quat2Rot (:41-54);
+// one thread per pair, fp64, same operation order as the reference's expressions
+__global__ void __launch_bounds__(256) quat_ops_kernel(int64_t B, const double* __restrict__ q1,
+                                                       const double* __restrict__ q2,
+                                                       double* __restrict__ prod, double* __restrict__ inv,
+                                                       double* __restrict__ rot) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const double w1 = q1[4 * b], x1 = q1[4 * b + 1], y1 = q1[4 * b + 2], z1 = q1[4 * b + 3];
+  if (prod) {
+    const double w2 = q2[4 * b], x2 = q2[4 * b + 1], y2 = q2[4 * b + 2], z2 = q2[4 * b + 3];
+    prod[4 * b] = w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2;
+    prod[4 * b + 1] = w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2;
+    prod[4 * b + 2] = w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2;
+    prod[4 * b + 3] = w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2;
+  }
+  if (inv) {
+    inv[4 * b] = w1;
+    inv[4 * b + 1] = -x1;
+    inv[4 * b + 2] = -y1;
+    inv[4 * b + 3] = -z1;
+  }
+  if (rot) {
+    double* R = rot + 9 * b;
+    R[0] = 2.0 * (w1 * w1 + x1 * x1) - 1.0;
+    R[1] = 2.0 * (x1 * y1 - w1 * z1);
+    R[2] = 2.0 * (x1 * z1 + w1 * y1);
+    R[3] = 2.0 * (x1 * y1 + w1 * z1);
+    R[4] = 2.0 * (w1 * w1 + y1 * y1) - 1.0;
+    R[5] = 2.0 * (y1 * z1 - w1 * x1);
+    R[6] = 2.0 * (x1 * z1 - w1 * y1);
+    R[7] = 2.0 * (y1 * z1 + w1 * x1);
+    R[8] = 2.0 * (w1 * w1 + z1 * z1) - 1.0;
+  }
+}
+
+hipError_t launch_quat_ops(int64_t B, const double* q1, const double* q2, double* prod, double* inv,
+                           double* rot, hipStream_t st) {
+  const int64_t grid = (B + 255) / 256;
+  hipLaunchKernelGGL(quat_ops_kernel, dim3((unsigned)grid), dim3(256), 0, st, B, q1, q2, prod, inv, rot);
+  return hipGetLastError();
+}
+
 #define MPCB_INST(T)                                                                              \
   template hipError_t launch_linearize<T>(int64_t, int, T, const Model<T>&, const T*, const T*,  \
                                           const T*, int64_t, T*, T*, T*, hipStream_t);           \

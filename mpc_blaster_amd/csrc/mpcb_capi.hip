@@ -628,6 +628,16 @@ extern "C" int mpcb_histogram(mpcb_handle* h, int64_t B, const void* u0, double 
   return MPCB_OK;
 }
 
+extern "C" int mpcb_quat_ops(int64_t B, const double* q1, const double* q2, double* prod, double* inv,
+                             double* rot, void* stream) {
+  if (B < 0) return fail(MPCB_E_INVALID, "B=%lld", (long long)B);
+  if (B == 0) return MPCB_OK;
+  if (!q1 || (prod && !q2)) return fail(MPCB_E_INVALID, "null quaternion array");
+  hipError_t e = launch_quat_ops(B, q1, q2, prod, inv, rot, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MPCB_E_HIP, "quat_ops launch: %s", hipGetErrorString(e));
+  return MPCB_OK;
+}
+
 extern "C" int mpcb_set_params(mpcb_handle* h, int64_t count, const void* params, int64_t params_sb,
                                int64_t params_kb) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");

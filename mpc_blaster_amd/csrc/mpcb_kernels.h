@@ -119,6 +119,8 @@ template <class T>
 hipError_t launch_gen_inputs(int64_t B, int N, T dt, uint64_t seed, uint64_t id_offset,
                              int ref_kind, T* x0, T* xref, int64_t xref_sb, T* uref,
                              int64_t uref_sb, T* wind, hipStream_t st);
+hipError_t launch_quat_ops(int64_t B, const double* q1, const double* q2, double* prod, double* inv,
+                           double* rot, hipStream_t st);
 template <class T>
 hipError_t launch_histogram(int64_t B, int nu, const T* u0, double lo, double hi, int nbins,
                             unsigned long long* counts, hipStream_t st);

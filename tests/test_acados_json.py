@@ -60,3 +60,16 @@ def test_rejects_unimplemented_solver_options():
     d['solver_options'] = dict(d['solver_options'], sim_method_num_stages=[2] * 60)
     with pytest.raises(ValueError, match='num_stages'):
         load_acados_ocp_json(d)
+
+
+def test_qp_iteration_cap_and_partial_box():
+    """qp_solver_iter_max (500 in the reference JSON) becomes the device's QP iteration
+    cap; a partial idxbu is refused rather than filled with +-1e20 rows."""
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        cfg, _ = load_acados_ocp_json(_nested())
+        assert cfg.max_as_iter == 500
+        d = _nested()
+        d['constraints'] = dict(d['constraints'], idxbu=[0, 1, 2, 3], lbu=[0.0] * 4, ubu=[65.0] * 4)
+        with pytest.raises(ValueError, match='idxbu'):
+            load_acados_ocp_json(d)

@@ -90,8 +90,8 @@ def test_rk4_sensitivities_match_central_differences():
 
 
 def test_mathutils_known_answers():
-    """utils/MathUtils.py helpers (unused by the path) vs our restatement."""
-    from mpc_blaster_amd.mathutils import quat_multiply, unit_quat_inverse, quat_to_rot
+    """utils/MathUtils.py helpers (unused by the path) vs the oracle restatement."""
+    from oracle.mathutils import quat_multiply, unit_quat_inverse, quat_to_rot
     d = np.load(os.path.join(GOLD, 'mathutils_ref.npz'))
     assert np.allclose(quat_multiply(d['q1'], d['q2']), d['prod'], atol=1e-14)
     assert np.allclose(unit_quat_inverse(d['q1']), d['inv'], atol=1e-15)

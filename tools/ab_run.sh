@@ -12,7 +12,7 @@ for rep in a b; do
   for v in base $V; do
     if [ $v = base ]; then unset MPCB_LIB; else export MPCB_LIB=$PWD/mpc_blaster_amd/variants/lib_$v.so; fi
     for w in $WL; do
-      timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary --workload $w > $O/${w}${rep}_$v.log 2>&1
+      timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary --no-latency --workload $w > $O/${w}${rep}_$v.log 2>&1
     done
   done
 done
