@@ -1,0 +1,524 @@
+// mpcb_as.hip — the input-box QP of the SQP_RTI step (thrust box lbu <= u <= ubu on stages
+// 0..N-1, blastermodel.py:259-270 / idxbu, JSON :11,86,148; BASELINE config c4), second design.
+//
+// Algorithm and iterates are those of the first active-set kernel (mpcb_box.hip PASS_BOX) and
+// of the oracle (oracle.ocp.pdas_solve): primal-dual active set with the Kim-Park block-principal
+// pivoting safeguard over P2's exported linearisation; the masked Riccati backward pass restarts
+// at the highest stage whose active set changed, from the value function P2 / the previous pass
+// stored there.  16 lanes per instance, lane j owning direction j, 4 instances per wavefront.
+//
+// What is new is how the 16 lanes of an instance exchange values.  The first kernel made every
+// exchange through LDS (write, read back: a ~100-cycle round trip on the serial chain of each
+// stage, three per forward stage) and measured ~7k cycles per forward stage and ~19k per
+// backward stage at c4 (tools/stamps.py c4).  Here each exchange is a DPP row broadcast inside
+// the FMA that consumes it (v_fmac_{f32,f64}_dpp ... row_newbcast:L reads lane L's operand):
+//   forward, per stage, no LDS at all:
+//     du_m  = kff_m + sum_{i<12} K[m][i] dx_i        input lanes, dx_i broadcast from state lane i
+//     acc_j = r0_j + sum_{l<16} row_j[l] z_l         every lane, z_l broadcast from lane l
+//   where a state lane's row is row i of [A|B] (r0 = gap: acc = dx'_i) and an input lane's row is
+//   row m of the stage Hessian [G_ux G_uu] (r0 = h_u: acc = the box multiplier mu_m), so one
+//   instruction stream serves both kinds of lane;
+//   backward, per stage: h = [A|B]^T (p + P gap), the stage cost, the 4x4 input block and the
+//   P update by broadcasts; only the transpose that keeps P symmetric goes through LDS.
+// Workspace pointers are formed once per lane (the stage-k record is base + k * stride), and the
+// active-set masks are kept per component by the input lanes (broadcast when the backward pass
+// needs all four) instead of in every lane.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "../../include/mpcb.h"
+#include "mpcb_kernels.h"
+#include "mpcb_split.h"
+
+#ifndef MPCB_AS_WAVES
+#define MPCB_AS_WAVES 2
+#endif
+
+namespace mpcb {
+namespace asq {
+
+// ---- DPP row broadcasts (16-lane rows = one instance) ---------------------------------------
+// Inline asm: the compiler's hazard recognizer does not look inside, so every block starts with
+// s_nop 4 (VALU / EXEC write -> DPP read wait states); no source is written inside a block.
+// Every block runs with all 16 lanes of each row active (group-uniform control flow only).
+#define ASQ_I(op, d, s, b, l) op " %" #d ", %" #s ", %" #b " row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+#define ASQ_A(op, d, s, b, l) op " %" #d ", |%" #s "|, |%" #b "| row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+// acc[l & 3] += bcast_l(%4) * %(5 + l)
+#define ASQ_DOT12(M, op)                                                                           \
+  M(op, 0, 4, 5, 0) M(op, 1, 4, 6, 1) M(op, 2, 4, 7, 2) M(op, 3, 4, 8, 3) M(op, 0, 4, 9, 4)       \
+  M(op, 1, 4, 10, 5) M(op, 2, 4, 11, 6) M(op, 3, 4, 12, 7) M(op, 0, 4, 13, 8) M(op, 1, 4, 14, 9)   \
+  M(op, 2, 4, 15, 10) M(op, 3, 4, 16, 11)
+#define ASQ_DOT16(M, op) ASQ_DOT12(M, op) M(op, 0, 4, 17, 12) M(op, 1, 4, 18, 13) M(op, 2, 4, 19, 14) M(op, 3, 4, 20, 15)
+#define ASQ_OUT4(acc) "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+#define ASQ_IN12(z, r) "v"(z), "v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), \
+                       "v"(r[7]), "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11])
+#define ASQ_IN16(z, r) ASQ_IN12(z, r), "v"(r[12]), "v"(r[13]), "v"(r[14]), "v"(r[15])
+
+// acc[*] += sum_{l<12} bcast_l(z) * r[l]
+__device__ __forceinline__ void dot12(float (&acc)[4], float z, const float (&r)[12]) {
+  asm("s_nop 4\n\t" ASQ_DOT12(ASQ_I, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
+}
+__device__ __forceinline__ void dot12(double (&acc)[4], double z, const double (&r)[12]) {
+  asm("s_nop 4\n\t" ASQ_DOT12(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
+}
+// acc[*] += sum_{l<16} bcast_l(z) * r[l]
+__device__ __forceinline__ void dot16(float (&acc)[4], float z, const float (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_I, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+__device__ __forceinline__ void dot16(double (&acc)[4], double z, const double (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+// acc[*] += sum_{l<16} |bcast_l(z) * r[l]|
+__device__ __forceinline__ void dot16abs(float (&acc)[4], float z, const float (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+__device__ __forceinline__ void dot16abs(double (&acc)[4], double z, const double (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+// acc[i] += bcast_i(a) * b, i < 12 (lane i's a feeds accumulator i); the fp64 form is
+// mpcb_split.h fmac12_diag
+#define ASQ_D(d, l) "v_fmac_f32_dpp %" #d ", %12, %13 row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void diag12(float (&acc)[12], float a, float b) {
+  asm("s_nop 4\n\t" ASQ_D(0, 0) ASQ_D(1, 1) ASQ_D(2, 2) ASQ_D(3, 3) ASQ_D(4, 4) ASQ_D(5, 5) ASQ_D(6, 6)
+      ASQ_D(7, 7) ASQ_D(8, 8) ASQ_D(9, 9) ASQ_D(10, 10) ASQ_D(11, 11)
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+        "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11])
+      : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void diag12(double (&acc)[12], double a, double b) { fmac12_diag(acc, a, b); }
+#undef ASQ_D
+
+template <class T> __device__ __forceinline__ T sum4(const T (&a)[4]) { return (a[0] + a[1]) + (a[2] + a[3]); }
+
+// lane L's value in every lane of its row (v_mov_b32_dpp row_newbcast:L)
+template <int L> __device__ __forceinline__ unsigned bcu(unsigned v) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xF, 0xF, true);
+}
+template <int L> __device__ __forceinline__ int bc(int v) { return (int)bcu<L>((unsigned)v); }
+template <int L> __device__ __forceinline__ float bc(float v) { return __uint_as_float(bcu<L>(__float_as_uint(v))); }
+template <int L> __device__ __forceinline__ uint64_t bc(uint64_t v) {
+  return ((uint64_t)bcu<L>((unsigned)(v >> 32)) << 32) | bcu<L>((unsigned)v);
+}
+template <int L> __device__ __forceinline__ double bc(double v) {
+  return __builtin_bit_cast(double, bc<L>(__builtin_bit_cast(uint64_t, v)));
+}
+
+// stage-invariant addressing of one quad-blocked workspace array (mpcb_split.h soa()):
+// element e of the stage-k record of this lane's instance = p0 + k * stride + e * SS
+template <class T> struct Arr {
+  T* p0;
+  int64_t stride;
+  __device__ __forceinline__ T* at(int k) const { return p0 + (int64_t)k * stride; }
+};
+template <class T> __device__ __forceinline__ Arr<T> arr(T* base, int rec, int64_t nq, int64_t c) {
+  return Arr<T>{base ? base + ((c >> 2) * rec) * SS + (c & (SS - 1)) : nullptr, nq * rec * SS};
+}
+
+template <class T>
+__device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
+  __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
+  const int lane = threadIdx.x;
+  const int q = lane >> 4;
+  const int j = lane & 15;
+  const int jx = j < NX ? j : 0;
+  const int ju = j >= NX ? j - NX : 0;
+  const bool stl = j < NX;                          // state lane (else input lane ju)
+  const uint64_t mst = lane_mask(stl);
+  T* const PX = lds_px[q];
+  const int64_t c_raw = (int64_t)blockIdx.x * GROUPS + q;
+  const bool valid = c_raw < a.nb;
+  const int64_t c = valid ? c_raw : a.nb - 1;       // inactive groups shadow the last instance
+  const int64_t nb = a.nb;
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const T h = a.h;
+  const Weights<T>& W = *a.W;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const T* xr = a.xref + b * a.xref_sb;
+  const T* ur = a.uref + b * a.uref_sb;
+  const T lbm = W.lbu[ju], ubm = W.ubu[ju];
+  constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
+  const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
+  const int64_t nq = (nb + SS - 1) / SS;
+  const Arr<T> XU = arr(a.XU, XU_REC, nq, c), AB = arr(a.AB, AB_REC, nq, c), ABT = arr(a.ABT, AB_REC, nq, c);
+  const Arr<T> GH = arr(a.GH, GH_REC, nq, c), KR = arr(a.KR, KR_REC, nq, c), PS = arr(a.PS, PS_REC, nq, c);
+  const Arr<T> GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
+  const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
+  // s * blkdiag(Q, R), column j (= row j): the stage cost of direction j
+  T swc[NZ];
+#pragma unroll
+  for (int i = 0; i < NZ; ++i) {
+    const T wq = (i < NX && stl) ? W.Q[i * NX + jx] : T(0);
+    const T wr = (i >= NX && !stl) ? W.R[(i - NX) * NU + ju] : T(0);
+    swc[i] = a.s * (wq + wr);
+  }
+  // row i of [A|B] at the constant columns (state lanes): position e_p, velocity e_v + h e_p
+  T crow[6];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    crow[p] = (jx == p) ? T(1) : T(0);
+    crow[3 + p] = ((jx == 6 + p) ? T(1) : T(0)) + ((jx == p) ? h : T(0));
+  }
+  const T* xrN = xr + (int64_t)N * NX;
+
+  uint64_t lowm = 0, upm = 0;   // input lanes: active sets of component ju, bit k = stage k
+  bool done = false;
+  int32_t st = MPCB_STATUS_OK;
+  int best = 0x7fffffff, pcount = 3;
+  int n_fwd = 0, n_bst = 0;
+  int kc = N - 1;               // highest stage whose active set changed (group-uniform)
+  for (int it = 0;; ++it) {
+    int kmax = kc;
+#pragma unroll
+    for (int g = 0; g < GROUPS; ++g) {
+      const int o = __builtin_amdgcn_readlane(kc, g * 16);
+      kmax = o > kmax ? o : kmax;
+    }
+    if (it > 0 && !done && kc >= 0) n_bst += kc + 1;
+    if (!done) ++n_fwd;
+    // ------------------------------------------------ masked Riccati over the cached [A|B]
+    if (it > 0 && kmax >= 0) {
+      T Pc[NX], pj;
+      {
+        const T vN = stl ? XU.at(N)[jx * SS] - xrN[jx] : T(0);
+        T qn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) qn[i] = stl ? W.QN[i * NX + jx] : T(0);
+        T acc[4] = {T(0), T(0), T(0), T(0)};
+        dot12(acc, vN, qn);
+        pj = stl ? sum4(acc) : T(0);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Pc[i] = qn[i];
+        if (kc >= 0 && kc < N - 1 && stl) {   // restart: the value function stored at kc + 1
+          const T* ps = PS.at(kc + 1) + jx * SS;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) Pc[i] = ps[i * NX * SS];
+          pj = ps[NX * NX * SS];
+        }
+      }
+      bool qp_ok = true;
+      // stage data one stage ahead: column j of [A|B], own (ybar - yref) and ybar components,
+      // own gap component
+      T ncol[NX], ne, nyb, ngp = T(0);
+      auto bload = [&](int k) {
+        if (tv >= 0) {
+          const T* ab = AB.at(k) + tv * SS;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) ncol[i] = ab[i * NVAR * SS];
+        } else {   // position / velocity directions: e_j, e_j + h e_{j-6}
+#pragma unroll
+          for (int i = 0; i < NX; ++i) ncol[i] = (i == j ? T(1) : T(0)) + ((j >= 6 && i == j - 6) ? h : T(0));
+        }
+        nyb = XU.at(k)[j * SS];
+        ne = nyb - (stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
+        if (iterate) ngp = stl ? GP.at(k)[jx * SS] : T(0);
+      };
+      bload(kmax);
+      for (int k = kmax; k >= 0; --k) {
+        const bool act = k <= kc;   // this group's stage is recomputed
+        T col[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) col[i] = ncol[i];
+        const T e = ne, yb = nyb, gpo = ngp;
+        if (k > 0) bload(k - 1);
+        // pt = p + P gap (component j), h = [A|B]^T pt
+        T pt = pj;
+        if (iterate) {
+          T acc[4] = {T(0), T(0), T(0), T(0)};
+          dot12(acc, gpo, Pc);
+          pt += stl ? sum4(acc) : T(0);
+        }
+        T hj;
+        T G[NZ];
+        if constexpr (sizeof(T) == 4) {
+          T acc[4] = {T(0), T(0), T(0), T(0)};
+          dot12(acc, pt, col);
+          hj = sum4(acc);
+          float y[16], g[16];
+          to_columns(outer12(Pc, col), y);   // lane (q,j): Y_q[:, j]  (P symmetric: row = column)
+          to_columns(outer12(col, y), g);    // lane (q,j): G_q[:, j]
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] = g[i];
+        } else {
+          double y[NX], g[NZ];
+          double hh = 0.0;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) y[i] = 0.0;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) g[i] = 0.0;
+          static_for<NX>([&](auto l) { fmac13_bc<decltype(l)::value>(y, hh, Pc, pt, col[l]); });
+#pragma unroll
+          for (int l = 0; l < NX; ++l) fmac16_diag(g, col[l], y[l]);
+          hj = hh;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] = g[i];
+        }
+        // stage cost: G += s blkdiag(Q, R), h += s blkdiag(Q, R) (ybar - yref)
+        {
+          T acc[4] = {hj, T(0), T(0), T(0)};
+          dot16(acc, e, swc);
+          hj = sum4(acc);
+        }
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) G[i] += swc[i];
+        if (act && valid && !stl) {   // unmasked input rows: the forward's multipliers
+          T* gh = GH.at(k) + ju * SS;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
+          gh[NZ * NU * SS] = hj;
+        }
+        // the 4x4 input block and h_u from the input lanes; masking of the fixed components
+        T Ht[NU * NU], ht[NU], Hux_t[NU];
+        static_for<NU>([&](auto mm) {
+          constexpr int m = decltype(mm)::value;
+          Ht[m * NU + 0] = bc<NX + 0>(G[NX + m]);
+          Ht[m * NU + 1] = bc<NX + 1>(G[NX + m]);
+          Ht[m * NU + 2] = bc<NX + 2>(G[NX + m]);
+          Ht[m * NU + 3] = bc<NX + 3>(G[NX + m]);
+          ht[m] = bc<NX + m>(hj);
+          Hux_t[m] = G[NX + m];
+        });
+        {
+          const bool lo = (lowm >> k) & 1ull, hi = (upm >> k) & 1ull;
+          const int fx_own = (!stl && (lo || hi)) ? 1 : 0;
+          const T dl_own = lo ? (lbm - yb) : (hi ? (ubm - yb) : T(0));   // input lanes: yb = ubar
+          int fixed[NU];
+          T delta[NU];
+          fixed[0] = bc<NX + 0>(fx_own); fixed[1] = bc<NX + 1>(fx_own);
+          fixed[2] = bc<NX + 2>(fx_own); fixed[3] = bc<NX + 3>(fx_own);
+          delta[0] = bc<NX + 0>(dl_own); delta[1] = bc<NX + 1>(dl_own);
+          delta[2] = bc<NX + 2>(dl_own); delta[3] = bc<NX + 3>(dl_own);
+          T hn[NU];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            T acc = ht[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) acc += fixed[n] ? Ht[m * NU + n] * delta[n] : T(0);
+            hn[m] = fixed[m] ? -delta[m] : acc;
+            Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
+          }
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            ht[m] = hn[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) {
+              const bool f = fixed[m] || fixed[n];
+              Ht[m * NU + n] = f ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+            }
+          }
+        }
+        T Lc[10];
+        chol4(Ht, Lc);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) ok = ok && (Lc[i] == Lc[i]);
+        qp_ok = qp_ok && (ok || !act);
+        T kff[NU], Kj[NU], nh[NU];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -ht[m];
+        chol4_solve(Lc, nh, kff);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -Hux_t[m];
+        chol4_solve(Lc, nh, Kj);
+        T pn = hj;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
+        // Pn[i] = G[i] + sum_m H_xu[i][m] K[m][j]; lane i owns H_xu[i][:] = its (unmasked) G[NX..]
+        T Pn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Pn[i] = G[i];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
+        if (act && valid) {
+          T* kr = KR.at(k);
+          if (stl) {
+#pragma unroll
+            for (int m = 0; m < NU; ++m) kr[(4 * j + m) * SS] = Kj[m];
+          } else {
+            kr[(4 * NX + ju) * SS] = sel<NU>(kff, ju);
+          }
+        }
+        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
+        if (stl) {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) PX[j * NX + i] = Pn[i];
+        }
+        wave_lds_sync();
+        {
+          const uint64_t ma = lane_mask(act);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            const T o = PX[i * NX + jx];
+            const T nv = csel(mst, csel(lane_mask(i <= j), Pn[i], o), T(0));
+            Pc[i] = csel(ma, nv, Pc[i]);
+          }
+          pj = csel(ma, csel(mst, pn, T(0)), pj);
+        }
+        wave_lds_sync();
+        if (act && valid && stl && k > 0) {   // snapshot P_k, p_k for a later restart
+          T* ps = PS.at(k) + j * SS;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) ps[i * NX * SS] = Pc[i];
+          ps[NX * NX * SS] = pj;
+        }
+      }
+      if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
+    }
+
+    // ------------------------------------------------ forward pass, multipliers, violations
+    uint64_t vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
+    const bool write = valid && !done;
+    T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
+    if (iterate && stl) zj = a.x0[b * a.x0_sb + jx] - XU.at(0)[jx * SS];
+    // stage data one stage ahead: own ybar component; state lanes: row jx of [A|B] (variable
+    // columns) and the gap; input lanes: row ju of (K | k) and, where component ju is fixed at
+    // the stage, row ju of the stage Hessian with h_u
+    T frow[NZ], fr0, fkr[NX], fkff, fyb;
+    auto fload = [&](int k) {
+      fyb = XU.at(k)[j * SS];
+      if (stl) {
+        const T* abt = ABT.at(k) + jx * SS;
+#pragma unroll
+        for (int t = 0; t < NVAR; ++t) frow[var_col(t)] = abt[t * NX * SS];
+        fr0 = iterate ? GP.at(k)[jx * SS] : T(0);
+      } else {
+        const T* kr = KR.at(k) + ju * SS;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) fkr[i] = kr[4 * i * SS];
+        fkff = kr[4 * NX * SS];
+        if (((lowm | upm) >> k) & 1ull) {
+          const T* gh = GH.at(k) + ju * SS;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) frow[i] = gh[i * NU * SS];
+          fr0 = gh[NZ * NU * SS];
+        }
+      }
+    };
+    fload(0);
+    for (int k = 0; k < N; ++k) {
+      T row[NZ], r0, krow[NX], kff, yb;
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) row[i] = frow[i];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) krow[i] = fkr[i];
+      r0 = fr0; kff = fkff; yb = fyb;
+      if (k + 1 < N) fload(k + 1);
+      // constant columns of the state rows
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        row[p] = csel(mst, crow[p], row[p]);
+        row[6 + p] = csel(mst, crow[3 + p], row[6 + p]);
+      }
+      // du = k + K dx (input lanes; dx_i broadcast from state lane i)
+      {
+        T acc[4] = {kff, T(0), T(0), T(0)};
+        dot12(acc, zj, krow);
+        zj = csel(mst, zj, sum4(acc));
+      }
+      const T yo = yb + zj;   // state lanes: x_k = xbar_k + dx_k; input lanes: u_k
+      if (write) {
+        if (stl) {
+          if (a.X) a.X[(b * (N + 1) + k) * NX + jx] = yo;
+        } else {
+          if (a.U) a.U[(b * N + k) * NU + ju] = yo;
+          if (k == 0) a.u0[b * NU + ju] = yo;
+        }
+      }
+      // every lane: r0 + row . z  (state lanes dx_{k+1}; input lanes the multiplier mu)
+      T acc[4] = {r0, T(0), T(0), T(0)};
+      dot16(acc, zj, row);
+      const T v = sum4(acc);
+      const bool lo = !stl && ((lowm >> k) & 1ull), hi = !stl && ((upm >> k) & 1ull);
+      T tol_mu = T(0);
+      if (__builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
+        T aa[4] = {fabs(r0), T(0), T(0), T(0)};
+        dot16abs(aa, zj, row);
+        tol_mu = T(64) * eps * sum4(aa);
+      }
+      if (!stl) {
+        const bool fr = !(lo || hi);
+        const T mu = v;
+        // violations beyond the rounding noise of u and mu (see mpcb_box.hip)
+        vlo |= (uint64_t)(fr && yo < lbm - tol_u) << k;
+        vhi |= (uint64_t)(fr && yo > ubm + tol_u) << k;
+        vfl |= (uint64_t)(lo && mu < -tol_mu) << k;
+        vfu |= (uint64_t)(hi && mu > tol_mu) << k;
+      } else {
+        zj = v;
+      }
+    }
+    if (write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+
+    // ------------------------------------------------ active-set update (Kim-Park)
+    const uint64_t V = vlo | vhi | vfl | vfu;
+    const int cnt = stl ? 0 : __popcll(V);
+    const int firstk = (!stl && V) ? __ffsll((long long)V) - 1 : 64;
+    int nV, first;
+    {
+      const int c0 = bc<NX + 0>(cnt), c1 = bc<NX + 1>(cnt), c2 = bc<NX + 2>(cnt), c3 = bc<NX + 3>(cnt);
+      nV = (c0 + c1) + (c2 + c3);
+      const int f0 = bc<NX + 0>(firstk) * NU + 0, f1 = bc<NX + 1>(firstk) * NU + 1;
+      const int f2 = bc<NX + 2>(firstk) * NU + 2, f3 = bc<NX + 3>(firstk) * NU + 3;
+      const int fa = f0 < f1 ? f0 : f1, fb = f2 < f3 ? f2 : f3;
+      first = fa < fb ? fa : fb;
+    }
+    const bool gconv = nV == 0;
+    const bool full = (nV < best) || (pcount > 0);
+    pcount = (nV < best) ? 3 : (full ? pcount - 1 : pcount);
+    best = nV < best ? nV : best;
+    const uint64_t selm =
+        full ? V : ((first < 64 * NU && (first % NU) == ju && !stl) ? (1ull << (first / NU)) : 0ull);
+    const uint64_t nlow = (lowm | (selm & vlo)) & ~(selm & vfl);
+    const uint64_t nup = (upm | (selm & vhi)) & ~(selm & vfu);
+    const uint64_t diff = stl ? 0ull : ((nlow ^ lowm) | (nup ^ upm));
+    uint64_t changed = (bc<NX + 0>(diff) | bc<NX + 1>(diff)) | (bc<NX + 2>(diff) | bc<NX + 3>(diff));
+    if (!done && !gconv) {
+      lowm = nlow;
+      upm = nup;
+    } else {
+      changed = 0;
+    }
+    // (the first masked pass is complete: P2 stored no snapshots)
+    kc = changed ? (it == 0 ? N - 1 : 63 - __clzll(changed)) : -1;
+    if (!done && gconv) done = true;
+    if (__all(done || !valid)) break;
+    if (it + 1 >= a.max_as_iter) {
+      if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+      break;
+    }
+  }
+  if (valid && j == NX) {
+    T u0c[NU];
+    load_vec<NU>(a.u0 + b * NU, u0c);
+    bool fin = true;
+#pragma unroll
+    for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+    // the QP status of the unconstrained pass (P2 wrote it) carries over
+    const int32_t st0 = a.status[b];
+    a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
+    if (a.qp_stats) {
+      a.qp_stats[2 * b] = n_fwd;
+      a.qp_stats[2 * b + 1] = n_bst;
+    }
+  }
+}
+
+}  // namespace asq
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS_WAVES, 8)))
+as_kernel_f32(SplitArgs<float> a) { asq::as_body<float>(a); }
+__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double>(a); }
+
+template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
+  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  if constexpr (sizeof(T) == 4)
+    hipLaunchKernelGGL(as_kernel_f32, dim3(g), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(as_kernel_f64, dim3(g), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+template hipError_t launch_as<double>(const SplitArgs<double>&, hipStream_t);
+template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
+
+}  // namespace mpcb

@@ -28,8 +28,10 @@ namespace mpcb {
 
 #ifdef MPCB_STAMPS
 // Diagnostic build only: per-region cycles of the 16-lane forward pass (PASS_FWD) of workgroup 0
-__device__ unsigned long long g_bstamps[8];
-#define BSTAMP(i) if constexpr (MODE == PASS_FWD) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); bst_acc[i] += t_ - bst_prev; bst_prev = t_; }
+// (PASS_BOX: [0..4] forward-stage regions over all passes, [5] masked backward passes, [6] the
+// forward tail, [7] active-set updates; [8] iterations, [9] backward stages run by the wave)
+__device__ unsigned long long g_bstamps[12];
+#define BSTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); bst_acc[i] += t_ - bst_prev; bst_prev = t_; }
 #else
 #define BSTAMP(i)
 #endif
@@ -88,7 +90,11 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
   // pass restarts at kc (group-uniform; N - 1 on the first masked pass) from the value function
   // snapshot P_{kc+1}, p_{kc+1} the previous pass stored (a.PS), and idles where k > kc.
   int kc = N - 1;
+#ifdef MPCB_STAMPS
+  unsigned long long bst_prev = __builtin_amdgcn_s_memtime(), bst_acc[12] = {};
+#endif
   for (int it = 0;; ++it) {
+    BSTAMP(7);
     // ------------------------------------------------ masked Riccati over the cached [A|B]
     // (iteration 0 is the unconstrained pass P2 already made: its gains are in KR)
     int kmax = kc;
@@ -99,6 +105,10 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     }
     if (BOX && it > 0 && !done && kc >= 0) n_bst += kc + 1;
     if (BOX && !done) ++n_fwd;
+#ifdef MPCB_STAMPS
+    bst_acc[8] += 1;
+    if (BOX && it > 0 && kmax >= 0) bst_acc[9] += kmax + 1;
+#endif
     if ((BOX ? it > 0 : MODE == PASS_SMALL) && kmax >= 0) {
       T pj = T(0);
       T Pc[NX];
@@ -319,6 +329,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
     }
 
+    BSTAMP(5);
     // ------------------------------------------------ forward pass, multipliers, violations
     uint64_t vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
     const bool write = valid && !done;
@@ -349,9 +360,6 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
         fa[sl][NZ] = iterate ? soa(a.GP, k, GP_REC, nb, c)[jx * SS] : T(0);
       }
     };
-#ifdef MPCB_STAMPS
-    unsigned long long bst_prev = __builtin_amdgcn_s_memtime(), bst_acc[8] = {};
-#endif
     auto stage = [&](int k, auto sl_tag) {
       constexpr int sl = decltype(sl_tag)::value;
       BSTAMP(0);
@@ -425,11 +433,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       if (DEPTH == 2 && k + 1 < N) stage(k + 1, S1());
     }
     if (write && a.X && j < NX) a.X[(b * (N + 1) + N) * NX + jx] = soa(a.XU, N, XU_REC, nb, c)[jx * SS] + dxj;
-#ifdef MPCB_STAMPS
-    if constexpr (MODE == PASS_FWD)
-      if (blockIdx.x == 0 && threadIdx.x == 0)
-        for (int i_ = 0; i_ < 8; ++i_) g_bstamps[i_] = bst_acc[i_];
-#endif
+    BSTAMP(6);
 
     if constexpr (!BOX) break;
     // ------------------------------------------------ active-set update (Kim-Park)
@@ -472,6 +476,10 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
       break;
     }
   }
+#ifdef MPCB_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int i_ = 0; i_ < 12; ++i_) g_bstamps[i_] = bst_acc[i_];
+#endif
   if (valid && j == NX) {
     T u0c[NU];
     load_vec<NU>(a.u0 + b * NU, u0c);
@@ -576,6 +584,6 @@ template hipError_t launch_fwd16<float>(const SplitArgs<float>&, hipStream_t);
 
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_stamps_box(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_bstamps), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_bstamps), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -2;
 }
 #endif

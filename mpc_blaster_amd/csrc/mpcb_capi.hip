@@ -65,6 +65,7 @@ struct mpcb_handle {
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
   int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
+  int as_dpp = 1;         // split path, input boxes: mpcb_as.hip (1) or mpcb_box.hip (0)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -243,6 +244,10 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     int64_t quad_max = 16384;   // the rollout with a lane quad per instance (latency-bound sizes)
     if (const char* e = getenv("MPCB_QUAD_P1_MAX")) quad_max = atoll(e);
     h->quad_p1 = (chunk <= quad_max) ? 1 : 0;
+    // input boxes: the DPP-exchange active-set kernel (mpcb_as.hip); MPCB_AS=0 selects the
+    // first (LDS-exchange) kernel of mpcb_box.hip
+    h->as_dpp = 1;
+    if (const char* e = getenv("MPCB_AS")) h->as_dpp = atoi(e) ? 1 : 0;
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
@@ -401,6 +406,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
       a.qp_stats = h->qp_stats;
+      a.as_dpp = h->as_dpp;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));

@@ -98,11 +98,13 @@ struct SplitArgs {
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
   int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
+  int as_dpp;        // input boxes: 1 = the DPP-exchange active-set kernel (mpcb_as.hip), 0 = mpcb_box.hip
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
                                            hipEvent_t* ev = nullptr);
 template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st);
+template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st);
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance

@@ -863,8 +863,8 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
   hipError_t e = hipSuccess;
-  if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_box.hip)
-    e = launch_box<T>(a, st);
+  if (a.GH)   // input boxes: active-set iterations over the exported linearisation
+    e = a.as_dpp ? launch_as<T>(a, st) : launch_box<T>(a, st);
   else if (a.fwd && a.fwd16)   // forward pass from the exported [A|B]^T, 16 lanes per instance
     e = launch_fwd16<T>(a, st);
   else if (a.fwd)

@@ -311,7 +311,10 @@ def test_full_size_c4_box_properties():
     st = m.get_status().clone()
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
-    assert (U >= -1e-4).all() and (U <= 65 + 1e-3).all()
+    # a free component is accepted up to the fp32 rounding band of the violation test beyond its
+    # bound: tol_u = 16 eps32 (|lb| + |ub| + 1) = 1.26e-4 (mpcb_as.hip / mpcb_box.hip)
+    tol_u = 16 * float(np.finfo(np.float32).eps) * 66.0
+    assert (U >= -tol_u).all() and (U <= 65 + tol_u).all()
     idx = np.arange(0, B, 2731)
     x0 = d['x0'][idx].double().cpu().numpy()
     xr = np.broadcast_to(d['xref'][0].double().cpu().numpy(), (len(idx), N + 1, 12)).copy()

@@ -14,10 +14,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mpc_blaster_amd import BatchedMPC, MPCConfig, _lib  # noqa: E402
 
 w = sys.argv[1] if len(sys.argv) > 1 else 'c2'
-B, dt, ref = (4096, 'f64', 'hover') if w == 'c2' else (65536, 'f32', 'sine')
-N = 20
-m = BatchedMPC(MPCConfig(N=N, dtype=dt), max_batch=B)
-d = m.gen_inputs(B, seed=1002, ref=ref)
+B, dt, ref = {'c2': (4096, 'f64', 'hover'), 'c3': (65536, 'f32', 'sine'), 'c4': (65536, 'f32', 'hover')}[w]
+N = 30 if w == 'c4' else 20
+box = dict(lbu=np.zeros(4), ubu=np.full(4, 65.0)) if w == 'c4' else {}
+m = BatchedMPC(MPCConfig(N=N, dtype=dt, **box), max_batch=B)
+d = m.gen_inputs(B, seed=1004 if w == 'c4' else 1002, ref=ref)
 for _ in range(3):
     m.solve(d['x0'], d['xref'], d['uref'], want_traj=True)
 torch.cuda.synchronize()
@@ -38,8 +39,23 @@ for n, x in zip(['u load + xu puts', 'rk4_nom (4 f + capture puts)', 'flush + sy
     print(f'   {n:32s} {x:9.0f}')
 print(f'   {"total":32s} {v1.sum():9.0f}')
 
-if hasattr(lib, 'mpcb_debug_stamps_box'):
-    ob = (ctypes.c_ulonglong * 8)()
+if hasattr(lib, 'mpcb_debug_stamps_box') and w == 'c4':
+    ob = (ctypes.c_ulonglong * 12)()
+    lib.mpcb_debug_stamps_box.argtypes = [ctypes.c_void_p]
+    assert lib.mpcb_debug_stamps_box(ob) == 0
+    v = np.array(ob[:], dtype=np.float64)
+    its, bst = v[8], v[9]
+    print(f'c4 active-set kernel, wave 0: {its:.0f} iterations, {bst:.0f} backward stages')
+    print(f'   backward cycles per stage           {v[5] / max(bst, 1):9.0f}   (total {v[5]:.0f})')
+    nf = its * N
+    for n, x in zip(['fwd: regs (+prefetch wait)', 'fwd: fload issue', 'fwd: du dot', 'fwd: publish du, read z',
+                     'fwd: outputs + dots + checks'], v[:5]):
+        print(f'   {n:36s} {x / nf:9.0f}   per forward stage')
+    print(f'   forward tail per pass               {v[6] / its:9.0f}')
+    print(f'   active-set update per iteration     {v[7] / its:9.0f}')
+    print(f'   total                               {v[:8].sum():9.0f}')
+elif hasattr(lib, 'mpcb_debug_stamps_box'):
+    ob = (ctypes.c_ulonglong * 12)()
     lib.mpcb_debug_stamps_box.argtypes = [ctypes.c_void_p]
     if lib.mpcb_debug_stamps_box(ob) == 0:
         vb = np.array(ob[:5], dtype=np.float64) / N
