@@ -38,6 +38,16 @@
 namespace mpcb {
 namespace asq {
 
+#ifdef MPCB_STAMPS
+// Diagnostic build only: per-region s_memtime cycles of workgroup 0, wave-summed over the whole
+// kernel ([0] backward init, [1..3] backward stage parts, [4..6] forward stage parts, [7] forward
+// tail + active-set update, [8] iterations, [9] backward stages), read by mpcb_debug_stamps_as()
+__device__ unsigned long long g_astamps[12];
+#define ASTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ast_acc[i] += t_ - ast_prev; ast_prev = t_; }
+#else
+#define ASTAMP(i)
+#endif
+
 // ---- DPP row broadcasts (16-lane rows = one instance) ---------------------------------------
 // Inline asm: the compiler's hazard recognizer does not look inside, so every block starts with
 // s_nop 4 (VALU / EXEC write -> DPP read wait states); no source is written inside a block.
@@ -111,11 +121,18 @@ template <class T> struct Arr {
   int64_t stride;
   __device__ __forceinline__ T* at(int k) const { return p0 + (int64_t)k * stride; }
 };
+// quad-blocked (soa) array: element e of the record at p0 + k * stride + e * SS
 template <class T> __device__ __forceinline__ Arr<T> arr(T* base, int rec, int64_t nq, int64_t c) {
   return Arr<T>{base ? base + ((c >> 2) * rec) * SS + (c & (SS - 1)) : nullptr, nq * rec * SS};
 }
+// row-major export (rec2): element e of the record at p0 + k * stride + e
+template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int64_t nq, int64_t c) {
+  return Arr<T>{base ? base + ((c >> 2) * SS + (c & (SS - 1))) * rec : nullptr, nq * SS * rec};
+}
 
-template <class T>
+// BOX: the active-set iterations; !BOX: one forward pass over P2's gains (unconstrained small
+// chunks, SplitArgs::fwd16)
+template <class T, bool BOX>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
   const int lane = threadIdx.x;
@@ -141,9 +158,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
   const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
   const int64_t nq = (nb + SS - 1) / SS;
-  const Arr<T> XU = arr(a.XU, XU_REC, nq, c), AB = arr(a.AB, AB_REC, nq, c), ABT = arr(a.ABT, AB_REC, nq, c);
-  const Arr<T> GH = arr(a.GH, GH_REC, nq, c), KR = arr(a.KR, KR_REC, nq, c), PS = arr(a.PS, PS_REC, nq, c);
-  const Arr<T> GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
+  const Arr<T> XU = arr(a.XU, XU_REC, nq, c), GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
+  const Arr<T> AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c), ABT = arr2(a.ABT, ABT2_REC, nq, c);
+  const Arr<T> GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c), KR = arr2(a.KR, KR2_REC, nq, c);
+  const Arr<T> PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
   // s * blkdiag(Q, R), column j (= row j): the stage cost of direction j
   T swc[NZ];
@@ -168,7 +186,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   int best = 0x7fffffff, pcount = 3;
   int n_fwd = 0, n_bst = 0;
   int kc = N - 1;               // highest stage whose active set changed (group-uniform)
+#ifdef MPCB_STAMPS
+  unsigned long long ast_prev = __builtin_amdgcn_s_memtime(), ast_acc[12] = {};
+#endif
   for (int it = 0;; ++it) {
+#ifdef MPCB_STAMPS
+    ast_acc[8] += 1;
+#endif
     int kmax = kc;
 #pragma unroll
     for (int g = 0; g < GROUPS; ++g) {
@@ -178,7 +202,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     if (it > 0 && !done && kc >= 0) n_bst += kc + 1;
     if (!done) ++n_fwd;
     // ------------------------------------------------ masked Riccati over the cached [A|B]
-    if (it > 0 && kmax >= 0) {
+    ASTAMP(7);
+    if (BOX && it > 0 && kmax >= 0) {
+#ifdef MPCB_STAMPS
+      ast_acc[9] += kmax + 1;
+#endif
       T Pc[NX], pj;
       {
         const T vN = stl ? XU.at(N)[jx * SS] - xrN[jx] : T(0);
@@ -191,10 +219,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) Pc[i] = qn[i];
         if (kc >= 0 && kc < N - 1 && stl) {   // restart: the value function stored at kc + 1
-          const T* ps = PS.at(kc + 1) + jx * SS;
+          T ps[16];
+          ldv<T, 16>(PS.at(kc + 1) + jx * 16, ps);
 #pragma unroll
-          for (int i = 0; i < NX; ++i) Pc[i] = ps[i * NX * SS];
-          pj = ps[NX * NX * SS];
+          for (int i = 0; i < NX; ++i) Pc[i] = ps[i];
+          pj = ps[NX];
         }
       }
       bool qp_ok = true;
@@ -203,9 +232,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       T ncol[NX], ne, nyb, ngp = T(0);
       auto bload = [&](int k) {
         if (tv >= 0) {
-          const T* ab = AB.at(k) + tv * SS;
-#pragma unroll
-          for (int i = 0; i < NX; ++i) ncol[i] = ab[i * NVAR * SS];
+          ldv<T, NX>(AB.at(k) + tv * NX, ncol);
         } else {   // position / velocity directions: e_j, e_j + h e_{j-6}
 #pragma unroll
           for (int i = 0; i < NX; ++i) ncol[i] = (i == j ? T(1) : T(0)) + ((j >= 6 && i == j - 6) ? h : T(0));
@@ -215,6 +242,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         if (iterate) ngp = stl ? GP.at(k)[jx * SS] : T(0);
       };
       bload(kmax);
+      ASTAMP(0);
       for (int k = kmax; k >= 0; --k) {
         const bool act = k <= kc;   // this group's stage is recomputed
         T col[NX];
@@ -262,11 +290,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         }
 #pragma unroll
         for (int i = 0; i < NZ; ++i) G[i] += swc[i];
+        ASTAMP(1);
         if (act && valid && !stl) {   // unmasked input rows: the forward's multipliers
-          T* gh = GH.at(k) + ju * SS;
+          T gr[20];
 #pragma unroll
-          for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
-          gh[NZ * NU * SS] = hj;
+          for (int i = 0; i < NZ; ++i) gr[i] = G[i];
+          gr[NZ] = hj;
+          gr[17] = gr[18] = gr[19] = T(0);
+          stv<T, 20>(GH.at(k) + ju * 20, gr);
         }
         // the 4x4 input block and h_u from the input lanes; masking of the fixed components
         T Ht[NU * NU], ht[NU], Hux_t[NU];
@@ -330,15 +361,16 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         for (int i = 0; i < NX; ++i) Pn[i] = G[i];
 #pragma unroll
         for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
-        if (act && valid) {
+        if (act && valid) {   // KR2: K[m][j] at 16 m + j, k_m at 16 m + 12
           T* kr = KR.at(k);
           if (stl) {
 #pragma unroll
-            for (int m = 0; m < NU; ++m) kr[(4 * j + m) * SS] = Kj[m];
+            for (int m = 0; m < NU; ++m) kr[m * 16 + j] = Kj[m];
           } else {
-            kr[(4 * NX + ju) * SS] = sel<NU>(kff, ju);
+            kr[ju * 16 + 12] = sel<NU>(kff, ju);
           }
         }
+        ASTAMP(2);
         // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
         if (stl) {
 #pragma unroll
@@ -357,11 +389,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         }
         wave_lds_sync();
         if (act && valid && stl && k > 0) {   // snapshot P_k, p_k for a later restart
-          T* ps = PS.at(k) + j * SS;
+          T ps[16];
 #pragma unroll
-          for (int i = 0; i < NX; ++i) ps[i * NX * SS] = Pc[i];
-          ps[NX * NX * SS] = pj;
+          for (int i = 0; i < NX; ++i) ps[i] = Pc[i];
+          ps[NX] = pj;
+          ps[13] = ps[14] = ps[15] = T(0);
+          stv<T, 16>(PS.at(k) + j * 16, ps);
         }
+        ASTAMP(3);
       }
       if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
     }
@@ -375,24 +410,25 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     // columns) and the gap; input lanes: row ju of (K | k) and, where component ju is fixed at
     // the stage, row ju of the stage Hessian with h_u
     T frow[NZ], fr0, fkr[NX], fkff, fyb;
+    // one 16-element vector load per lane for the row of either kind (a state lane's ABT2 row
+    // is 12 long: its last 4 elements belong to the next row or record, or to the workspace
+    // padding, and are not used)
     auto fload = [&](int k) {
       fyb = XU.at(k)[j * SS];
-      if (stl) {
-        const T* abt = ABT.at(k) + jx * SS;
+      T v[16];
+      ldv<T, 16>(stl ? ABT.at(k) + jx * 12 : KR.at(k) + ju * 16, v);
 #pragma unroll
-        for (int t = 0; t < NVAR; ++t) frow[var_col(t)] = abt[t * NX * SS];
-        fr0 = iterate ? GP.at(k)[jx * SS] : T(0);
-      } else {
-        const T* kr = KR.at(k) + ju * SS;
+      for (int t = 0; t < NVAR; ++t) frow[var_col(t)] = v[t];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) fkr[i] = kr[4 * i * SS];
-        fkff = kr[4 * NX * SS];
-        if (((lowm | upm) >> k) & 1ull) {
-          const T* gh = GH.at(k) + ju * SS;
+      for (int i = 0; i < NX; ++i) fkr[i] = v[i];
+      fkff = v[NX];
+      fr0 = (stl && iterate) ? v[NVAR] : T(0);
+      if (BOX && (((lowm | upm) >> k) & 1ull)) {   // input lanes: component ju fixed at stage k
+        T g[20];
+        ldv<T, 20>(GH.at(k) + ju * 20, g);
 #pragma unroll
-          for (int i = 0; i < NZ; ++i) frow[i] = gh[i * NU * SS];
-          fr0 = gh[NZ * NU * SS];
-        }
+        for (int i = 0; i < NZ; ++i) frow[i] = g[i];
+        fr0 = g[NZ];
       }
     };
     fload(0);
@@ -403,7 +439,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
       for (int i = 0; i < NX; ++i) krow[i] = fkr[i];
       r0 = fr0; kff = fkff; yb = fyb;
+      ASTAMP(7);
       if (k + 1 < N) fload(k + 1);
+      ASTAMP(4);
       // constant columns of the state rows
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -425,13 +463,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           if (k == 0) a.u0[b * NU + ju] = yo;
         }
       }
+      ASTAMP(5);
       // every lane: r0 + row . z  (state lanes dx_{k+1}; input lanes the multiplier mu)
       T acc[4] = {r0, T(0), T(0), T(0)};
       dot16(acc, zj, row);
       const T v = sum4(acc);
       const bool lo = !stl && ((lowm >> k) & 1ull), hi = !stl && ((upm >> k) & 1ull);
       T tol_mu = T(0);
-      if (__builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
+      if (BOX && __builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
         T aa[4] = {fabs(r0), T(0), T(0), T(0)};
         dot16abs(aa, zj, row);
         tol_mu = T(64) * eps * sum4(aa);
@@ -447,8 +486,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       } else {
         zj = v;
       }
+      ASTAMP(6);
     }
     if (write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+    if constexpr (!BOX) break;
 
     // ------------------------------------------------ active-set update (Kim-Park)
     const uint64_t V = vlo | vhi | vfl | vfu;
@@ -488,6 +529,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       break;
     }
   }
+#ifdef MPCB_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
+#endif
   if (valid && j == NX) {
     T u0c[NU];
     load_vec<NU>(a.u0 + b * NU, u0c);
@@ -497,7 +542,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     // the QP status of the unconstrained pass (P2 wrote it) carries over
     const int32_t st0 = a.status[b];
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
-    if (a.qp_stats) {
+    if (BOX && a.qp_stats) {
       a.qp_stats[2 * b] = n_fwd;
       a.qp_stats[2 * b + 1] = n_bst;
     }
@@ -507,8 +552,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 }  // namespace asq
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS_WAVES, 8)))
-as_kernel_f32(SplitArgs<float> a) { asq::as_body<float>(a); }
-__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double>(a); }
+as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true>(a); }
+__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true>(a); }
+template <class T>
+__global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false>(a); }
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
@@ -518,7 +565,21 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
     hipLaunchKernelGGL(as_kernel_f64, dim3(g), dim3(64), 0, st, a);
   return hipGetLastError();
 }
+// forward pass of the unconstrained small-chunk path from P2's row-major exports (ABT2, KR2)
+template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st) {
+  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+template hipError_t launch_fwd_rm<double>(const SplitArgs<double>&, hipStream_t);
+template hipError_t launch_fwd_rm<float>(const SplitArgs<float>&, hipStream_t);
 template hipError_t launch_as<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb
+
+#ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_stamps_as(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_astamps), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -65,7 +65,6 @@ struct mpcb_handle {
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
   int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
-  int as_dpp = 1;         // split path, input boxes: mpcb_as.hip (1) or mpcb_box.hip (0)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -244,14 +243,11 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     int64_t quad_max = 16384;   // the rollout with a lane quad per instance (latency-bound sizes)
     if (const char* e = getenv("MPCB_QUAD_P1_MAX")) quad_max = atoll(e);
     h->quad_p1 = (chunk <= quad_max) ? 1 : 0;
-    // input boxes: the DPP-exchange active-set kernel (mpcb_as.hip); MPCB_AS=0 selects the
-    // first (LDS-exchange) kernel of mpcb_box.hip
-    h->as_dpp = 1;
-    if (const char* e = getenv("MPCB_AS")) h->as_dpp = atoi(e) ? 1 : 0;
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
-    h->chunk_elems = per * ((chunk + 3) / 4 * 4);
+    // (+64: the 16-lane forward's 16-element row loads may read past the last ABT2 row)
+    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
   fill_model(*cfg, Jinv, h->Md);
@@ -396,17 +392,19 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.XU = base;
       a.CC = a.XU + (int64_t)(N + 1) * nbp * XU_REC;
       a.KR = a.CC + (int64_t)N * nbp * CCS_REC;
-      a.GP = a.KR + (int64_t)N * nbp * KR_REC;
+      a.GP = a.KR + (int64_t)N * nbp * KR2_REC;
       a.small = h->small;
       a.fwd16 = h->fwd16;
       a.quad_p1 = h->quad_p1;
       T* ab = a.GP + (int64_t)N * nbp * GP_REC;
+      // row-major exports for the active-set kernel and the 16-lane forward pass; the optional
+      // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
+      a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
       a.AB = (h->cfg.box_u || h->small) ? ab : nullptr;
-      a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB_REC : nullptr;
-      a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * AB_REC : nullptr;
-      a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH_REC : nullptr;
+      a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
+      a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
+      a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH2_REC : nullptr;
       a.qp_stats = h->qp_stats;
-      a.as_dpp = h->as_dpp;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));

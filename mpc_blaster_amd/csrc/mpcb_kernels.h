@@ -72,6 +72,16 @@ constexpr int NVAR = 10;
 __host__ __device__ constexpr int var_col(int t) { return t < 3 ? 3 + t : 6 + t; }
 __host__ __device__ constexpr int var_index(int j) { return (j >= 3 && j < 6) ? j - 3 : (j >= 9 ? j - 6 : -1); }
 constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
+// Row-major exports (SplitArgs::rm = 1: the input-box kernel mpcb_as.hip and the 16-lane forward
+// pass of small unconstrained chunks).  Per stage the 4 instances of a quad follow each other and
+// each instance's record is contiguous, so a lane's row (or column) is a run of 16-B-aligned
+// vectors (mpcb_split.h rec2()):
+//   AB2  [10][12]  column var_col(t) of [A|B], 12 entries       (backward: lane var_col(t))
+//   ABT2 [12][12]  row i of [A|B] at the variable columns t < 10, slot 10 = gap_i (iterate)
+//   KR2  [4][16]   row m of K (12 entries), slot 12 = k_m
+//   GH2  [4][20]   row m of the stage Hessian's input rows (16 entries), slot 16 = h_u[m]
+//   PS2  [12][16]  column j of P_k (12 entries), slot 12 = p_k[j]
+constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * 12, KR2_REC = 4 * 16, GH2_REC = 4 * 20, PS2_REC = 12 * 16;
 
 template <class T>
 struct SplitArgs {
@@ -98,13 +108,14 @@ struct SplitArgs {
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
   int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
-  int as_dpp;        // input boxes: 1 = the DPP-exchange active-set kernel (mpcb_as.hip), 0 = mpcb_box.hip
+  int rm;            // 1: P2 writes the row-major exports (AB2, ABT2, GH2, KR2 in a.AB/a.ABT/a.GH/a.KR)
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
                                            hipEvent_t* ev = nullptr);
 template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st);
+template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st);
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance

@@ -122,4 +122,38 @@ __device__ __forceinline__ T* soa(T* base, int k, int rec, int64_t nb, int64_t c
   return base + (((int64_t)k * nq + (c >> 2)) * rec) * SS + (c & (SS - 1));
 }
 
+// Row-major export records (mpcb_kernels.h AB2_REC ...): record of chunk instance c at stage k.
+template <class T>
+__device__ __forceinline__ T* rec2(T* base, int k, int rec, int64_t nb, int64_t c) {
+  const int64_t nq = (nb + SS - 1) / SS;
+  return base + (((int64_t)k * nq + (c >> 2)) * SS + (c & (SS - 1))) * rec;
+}
+
+// n contiguous elements through 16-B vector accesses (p 16-B aligned, n * sizeof(T) % 16 == 0)
+template <class T, int n> __device__ __forceinline__ void ldv(const T* __restrict__ p, T* v) {
+  constexpr int W = 16 / sizeof(T);
+  static_assert((n % W) == 0, "ldv: whole 16-B vectors");
+  typedef T V __attribute__((ext_vector_type(W)));
+  const V* vp = reinterpret_cast<const V*>(p);
+#pragma unroll
+  for (int c = 0; c < n / W; ++c) {
+    const V x = vp[c];
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[c * W + e] = x[e];
+  }
+}
+template <class T, int n> __device__ __forceinline__ void stv(T* __restrict__ p, const T* v) {
+  constexpr int W = 16 / sizeof(T);
+  static_assert((n % W) == 0, "stv: whole 16-B vectors");
+  typedef T V __attribute__((ext_vector_type(W)));
+  V* vp = reinterpret_cast<V*>(p);
+#pragma unroll
+  for (int c = 0; c < n / W; ++c) {
+    V x;
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = v[c * W + e];
+    vp[c] = x;
+  }
+}
+
 }  // namespace mpcb

@@ -439,15 +439,27 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       rk4_tan<T>(cc, dx, du, a.h, a.M, col);
       STAMP(1);
       const int tv = var_index(j);   // exported: the state-dependent columns only
-      if (EXPORT && a.AB && valid && tv >= 0) {
-        T* ab = soa(a.AB, k, AB_REC, nb, c);
+      if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
+        if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c) + tv * NX, col);
+        if (a.ABT && valid) {
+          T* abt = rec2(a.ABT, k, ABT2_REC, nb, c);
+          if (tv >= 0) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) ab[(i * NVAR + tv) * SS] = col[i];
-      }
-      if (EXPORT && a.ABT && valid && tv >= 0) {
-        T* abt = soa(a.ABT, k, AB_REC, nb, c);
+            for (int i = 0; i < NX; ++i) abt[i * 12 + tv] = col[i];
+          }
+          if (iterate && j < NX) abt[j * 12 + NVAR] = cc[CCS_REC + j];   // gap_j
+        }
+      } else {
+        if (EXPORT && a.AB && valid && tv >= 0) {
+          T* ab = soa(a.AB, k, AB_REC, nb, c);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) abt[(tv * NX + i) * SS] = col[i];
+          for (int i = 0; i < NX; ++i) ab[(i * NVAR + tv) * SS] = col[i];
+        }
+        if (EXPORT && a.ABT && valid && tv >= 0) {
+          T* abt = soa(a.ABT, k, AB_REC, nb, c);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) abt[(tv * NX + i) * SS] = col[i];
+        }
       }
       T pt = pj;
       if (iterate) {
@@ -518,11 +530,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       G[i] += w;
       hj += w * L.v[i];
     }
-    if (EXPORT && a.GH && valid && j >= NX) {
-      T* gh = soa(a.GH, k, GH_REC, nb, c) + ju * SS;
+    if (EXPORT && a.GH && valid && j >= NX) {   // box path: always row-major (GH2)
+      T row[20];
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) gh[i * NU * SS] = G[i];
-      gh[NZ * NU * SS] = hj;
+      for (int i = 0; i < NZ; ++i) row[i] = G[i];
+      row[NZ] = hj;
+      row[17] = row[18] = row[19] = T(0);
+      stv<T, 20>(rec2(a.GH, k, GH2_REC, nb, c) + ju * 20, row);
     }
 #pragma unroll
     for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
@@ -570,7 +584,15 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     STAMP(6);
     kff0 = sel<NU>(kff, ju);
-    if (valid) {
+    if (valid && a.rm) {   // KR2: K[m][j] at 16 m + j, k_m at 16 m + 12
+      T* kr = rec2(a.KR, k, KR2_REC, nb, c);
+      if (j < NX) {
+#pragma unroll
+        for (int m = 0; m < NU; ++m) kr[m * 16 + j] = Kj[m];
+      } else {
+        kr[ju * 16 + 12] = kff0;
+      }
+    } else if (valid) {
       // K[m][j] at 4j + m (state lanes), kff[m] at 4*NX + m (input lanes): the first store is
       // common to both kinds of lane
       T* kr = soa(a.KR, k, KR_REC, nb, c);
@@ -802,8 +824,11 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
 }
 
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box) {
-  return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR_REC + (iterate ? GP_REC : 0)) +
-         (box == 2 ? (int64_t)N * (2 * AB_REC + GH_REC + PS_REC) : box == 1 ? (int64_t)N * 2 * AB_REC : 0);
+  // (KR sized for the larger of its two layouts; box == 1: the old [A|B] pair of the small path or
+  // ABT2 of the 16-lane forward)
+  return (int64_t)(N + 1) * XU_REC + (int64_t)N * (CCS_REC + KR2_REC + (iterate ? GP_REC : 0)) +
+         (box == 2 ? (int64_t)N * (AB2_REC + ABT2_REC + GH2_REC + PS2_REC)
+                   : box == 1 ? (int64_t)N * (AB_REC + ABT2_REC) : 0);
 }
 
 template <class T>
@@ -863,10 +888,10 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
   hipError_t e = hipSuccess;
-  if (a.GH)   // input boxes: active-set iterations over the exported linearisation
-    e = a.as_dpp ? launch_as<T>(a, st) : launch_box<T>(a, st);
+  if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_as.hip)
+    e = launch_as<T>(a, st);
   else if (a.fwd && a.fwd16)   // forward pass from the exported [A|B]^T, 16 lanes per instance
-    e = launch_fwd16<T>(a, st);
+    e = launch_fwd_rm<T>(a, st);
   else if (a.fwd)
     e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
   if (ev) (void)hipEventRecord(ev[3], st);

@@ -39,7 +39,23 @@ for n, x in zip(['u load + xu puts', 'rk4_nom (4 f + capture puts)', 'flush + sy
     print(f'   {n:32s} {x:9.0f}')
 print(f'   {"total":32s} {v1.sum():9.0f}')
 
-if hasattr(lib, 'mpcb_debug_stamps_box') and w == 'c4':
+if hasattr(lib, 'mpcb_debug_stamps_as') and w == 'c4' and os.environ.get('MPCB_AS', '1') != '0':
+    ob = (ctypes.c_ulonglong * 12)()
+    lib.mpcb_debug_stamps_as.argtypes = [ctypes.c_void_p]
+    assert lib.mpcb_debug_stamps_as(ob) == 0
+    v = np.array(ob[:], dtype=np.float64)
+    its, bst = v[8], v[9]
+    nf = its * N
+    print(f'c4 active-set kernel v2 (mpcb_as.hip), wave 0: {its:.0f} iterations, {bst:.0f} backward stages')
+    print(f'   backward init per pass                 {v[0] / max(its - 1, 1):9.0f}')
+    for n, x in zip(['bwd: loads, h, products, stage cost', 'bwd: input block, masking, Cholesky, P, stores',
+                     'bwd: P transpose, snapshot'], v[1:4]):
+        print(f'   {n:44s} {x / max(bst, 1):9.0f}   per backward stage')
+    for n, x in zip(['fwd: prefetch issue', 'fwd: du, outputs', 'fwd: row dot, multiplier checks'], v[4:7]):
+        print(f'   {n:44s} {x / nf:9.0f}   per forward stage')
+    print(f'   {"fwd copy + tail + active-set updates":44s} {v[7] / its:9.0f}   per iteration')
+    print(f'   total {v[:8].sum():.0f}')
+elif hasattr(lib, 'mpcb_debug_stamps_box') and w == 'c4':
     ob = (ctypes.c_ulonglong * 12)()
     lib.mpcb_debug_stamps_box.argtypes = [ctypes.c_void_p]
     assert lib.mpcb_debug_stamps_box(ob) == 0
