@@ -34,6 +34,12 @@
 #ifndef MPCB_AS_WAVES
 #define MPCB_AS_WAVES 2
 #endif
+#ifndef MPCB_AS_FDEPTH   // forward-pass prefetch ring (stages): active-set kernel
+#define MPCB_AS_FDEPTH 1
+#endif
+#ifndef MPCB_FWD_FDEPTH  // the same for the unconstrained forward pass (fwd_rm_kernel)
+#define MPCB_FWD_FDEPTH 2
+#endif
 
 namespace mpcb {
 namespace asq {
@@ -132,9 +138,17 @@ template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int6
 
 // BOX: the active-set iterations; !BOX: one forward pass over P2's gains (unconstrained small
 // chunks, SplitArgs::fwd16)
+// Output staging: a pass's X / U rows go to LDS (one [(N+1)*12 | N*4] block per instance) and
+// leave as 16-B vector stores after the pass.  Stores issued inside the stage loop would sit in
+// the same in-order vmcnt queue as the prefetch loads, so every wait for a prefetched row also
+// waited for the write acknowledgements of the previous stages' scattered 4/8-B output stores.
+constexpr int OUT_NMAX = 64;   // longer horizons store directly
+template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
+
 template <class T, bool BOX>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
+  extern __shared__ __attribute__((aligned(16))) unsigned char as_dyn[];
   const int lane = threadIdx.x;
   const int q = lane >> 4;
   const int j = lane & 15;
@@ -163,14 +177,16 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   const Arr<T> GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c), KR = arr2(a.KR, KR2_REC, nq, c);
   const Arr<T> PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
-  // s * blkdiag(Q, R), column j (= row j): the stage cost of direction j
-  T swc[NZ];
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) {
-    const T wq = (i < NX && stl) ? W.Q[i * NX + jx] : T(0);
-    const T wr = (i >= NX && !stl) ? W.R[(i - NX) * NU + ju] : T(0);
-    swc[i] = a.s * (wq + wr);
+  // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
+  // the stage cost of direction j, when a backward stage needs it
+  __shared__ T SW[NZ * NZ];
+  for (int e = lane; e < NZ * NZ; e += 64) {
+    const int r = e / NZ, cl = e % NZ;
+    const T wq = (r < NX && cl < NX) ? W.Q[r * NX + cl] : T(0);
+    const T wr = (r >= NX && cl >= NX) ? W.R[(r - NX) * NU + (cl - NX)] : T(0);
+    SW[e] = a.s * (wq + wr);
   }
+  wave_lds_sync();
   // row i of [A|B] at the constant columns (state lanes): position e_p, velocity e_v + h e_p
   T crow[6];
 #pragma unroll
@@ -284,12 +300,15 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         }
         // stage cost: G += s blkdiag(Q, R), h += s blkdiag(Q, R) (ybar - yref)
         {
+          T swc[NZ];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) swc[i] = SW[i * NZ + j];
           T acc[4] = {hj, T(0), T(0), T(0)};
           dot16(acc, e, swc);
           hj = sum4(acc);
-        }
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) G[i] += swc[i];
+          for (int i = 0; i < NZ; ++i) G[i] += swc[i];
+        }
         ASTAMP(1);
         if (act && valid && !stl) {   // unmasked input rows: the forward's multipliers
           T gr[20];
@@ -404,58 +423,70 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     // ------------------------------------------------ forward pass, multipliers, violations
     uint64_t vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
     const bool write = valid && !done;
+    // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
+    const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
+    T* const xs = reinterpret_cast<T*>(as_dyn) + q * out_elems<T>(N);   // X rows, then U rows
+    T* const us = xs + (N + 1) * NX;
     T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
     if (iterate && stl) zj = a.x0[b * a.x0_sb + jx] - XU.at(0)[jx * SS];
-    // stage data one stage ahead: own ybar component; state lanes: row jx of [A|B] (variable
-    // columns) and the gap; input lanes: row ju of (K | k) and, where component ju is fixed at
-    // the stage, row ju of the stage Hessian with h_u
-    T frow[NZ], fr0, fkr[NX], fkff, fyb;
-    // one 16-element vector load per lane for the row of either kind (a state lane's ABT2 row
-    // is 12 long: its last 4 elements belong to the next row or record, or to the workspace
-    // padding, and are not used)
-    auto fload = [&](int k) {
-      fyb = XU.at(k)[j * SS];
-      T v[16];
-      ldv<T, 16>(stl ? ABT.at(k) + jx * 12 : KR.at(k) + ju * 16, v);
-#pragma unroll
-      for (int t = 0; t < NVAR; ++t) frow[var_col(t)] = v[t];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) fkr[i] = v[i];
-      fkff = v[NX];
-      fr0 = (stl && iterate) ? v[NVAR] : T(0);
-      if (BOX && (((lowm | upm) >> k) & 1ull)) {   // input lanes: component ju fixed at stage k
-        T g[20];
-        ldv<T, 20>(GH.at(k) + ju * 20, g);
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) frow[i] = g[i];
-        fr0 = g[NZ];
-      }
+    // Stage data FD stages ahead in a ring of register slots (the stage loop is unrolled by FD so
+    // every slot is a fixed register set, loaded at the end of the stage that consumed it and used
+    // FD - 1 stages later): own ybar component; one row (a state lane's ABT2 row: the variable
+    // columns of row jx of [A|B] and the gap; an input lane's KR2 row: row ju of K and k_ju);
+    // input lanes whose component is fixed
+    // at the stage: row ju of the stage Hessian with h_u.  The raw vectors stay in the slot until
+    // use: moving them on arrival would make the compiler wait for the loads right away.
+    // (The Hessian rows, needed at few stages, come one stage ahead through a single slot.)
+    constexpr int FD = BOX ? MPCB_AS_FDEPTH : MPCB_FWD_FDEPTH;
+    constexpr int FL = sizeof(T) == 8 ? 14 : 16;
+    T pv[FD][FL], pyb[FD], pg[20];
+    auto rload = [&](int k, auto slot_tag) {
+      constexpr int sl = decltype(slot_tag)::value;
+      pyb[sl] = XU.at(k)[j * SS];
+      // one load for both kinds of lane, from a per-lane address: the 13 elements an input lane
+      // uses rounded up to 16-B vectors (14 in fp64, 16 in fp32); a state lane's 12-element
+      // ABT2 row is followed by the next row or record, or by the workspace padding
+      ldv<T, FL>(stl ? ABT.at(k) + jx * 12 : KR.at(k) + ju * 16, pv[sl]);
     };
-    fload(0);
-    for (int k = 0; k < N; ++k) {
-      T row[NZ], r0, krow[NX], kff, yb;
+    auto gload = [&](int k) {
+      if (BOX && (((lowm | upm) >> k) & 1ull)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
+    };
+    static_for<FD>([&](auto s) {
+      if (decltype(s)::value < N) rload(decltype(s)::value, s);
+    });
+    gload(0);
+    auto stage = [&](int k, auto slot_tag) {
+      constexpr int sl = decltype(slot_tag)::value;
+      const bool fixk = BOX && (((lowm | upm) >> k) & 1ull);   // input lanes: ju fixed at stage k
+      const uint64_t mfix = lane_mask(fixk);
+      T row[NZ];
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) row[i] = frow[i];
+      for (int i = 0; i < NZ; ++i) row[i] = BOX ? csel(mfix, pg[i], T(0)) : T(0);
 #pragma unroll
-      for (int i = 0; i < NX; ++i) krow[i] = fkr[i];
-      r0 = fr0; kff = fkff; yb = fyb;
-      ASTAMP(7);
-      if (k + 1 < N) fload(k + 1);
-      ASTAMP(4);
+      for (int t = 0; t < NVAR; ++t) row[var_col(t)] = csel(mst, pv[sl][t], row[var_col(t)]);
       // constant columns of the state rows
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         row[p] = csel(mst, crow[p], row[p]);
         row[6 + p] = csel(mst, crow[3 + p], row[6 + p]);
       }
+      const T r0 = csel(mst, iterate ? pv[sl][NVAR] : T(0), BOX ? csel(mfix, pg[NZ], T(0)) : T(0));
+      const T yb = pyb[sl];
+      ASTAMP(4);
       // du = k + K dx (input lanes; dx_i broadcast from state lane i)
       {
-        T acc[4] = {kff, T(0), T(0), T(0)};
+        T acc[4] = {pv[sl][NX], T(0), T(0), T(0)};
+        T krow[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) krow[i] = pv[sl][i];
         dot12(acc, zj, krow);
         zj = csel(mst, zj, sum4(acc));
       }
       const T yo = yb + zj;   // state lanes: x_k = xbar_k + dx_k; input lanes: u_k
-      if (write) {
+      if (stage_out) {
+        if (stl) xs[k * NX + jx] = yo;
+        else us[k * NU + ju] = yo;
+      } else if (write) {
         if (stl) {
           if (a.X) a.X[(b * (N + 1) + k) * NX + jx] = yo;
         } else {
@@ -471,7 +502,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       const bool lo = !stl && ((lowm >> k) & 1ull), hi = !stl && ((upm >> k) & 1ull);
       T tol_mu = T(0);
       if (BOX && __builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
-        T aa[4] = {fabs(r0), T(0), T(0), T(0)};
+        T aa[4] = {T(fabs(r0)), T(0), T(0), T(0)};
         dot16abs(aa, zj, row);
         tol_mu = T(64) * eps * sum4(aa);
       }
@@ -486,9 +517,38 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       } else {
         zj = v;
       }
+      if (k + FD < N) rload(k + FD, slot_tag);   // refill this slot FD stages ahead
+      if (k + 1 < N) gload(k + 1);
       ASTAMP(6);
+    };
+    for (int k0 = 0; k0 < N; k0 += FD) {
+      static_for<FD>([&](auto s) {
+        if (k0 + decltype(s)::value < N) stage(k0 + decltype(s)::value, s);
+      });
     }
-    if (write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+    if (stage_out) {
+      if (stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
+      wave_lds_sync();
+      if (write) {   // the group's X block and U block are contiguous in the outputs
+        constexpr int V = 16 / sizeof(T);
+        typedef T Vec __attribute__((ext_vector_type(V)));
+        const int nx = (N + 1) * NX, nu = N * NU;
+        if (a.X) {
+          Vec* dst = reinterpret_cast<Vec*>(a.X + b * nx);
+          const Vec* src = reinterpret_cast<const Vec*>(xs);
+          for (int t = j; t < nx / V; t += NZ) dst[t] = src[t];
+        }
+        if (a.U) {
+          Vec* dst = reinterpret_cast<Vec*>(a.U + b * nu);
+          const Vec* src = reinterpret_cast<const Vec*>(us);
+          for (int t = j; t < nu / V; t += NZ) dst[t] = src[t];
+        }
+        if (!stl) a.u0[b * NU + ju] = us[ju];
+      }
+      wave_lds_sync();
+    } else if (write && a.X && stl) {
+      a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+    }
     if constexpr (!BOX) break;
 
     // ------------------------------------------------ active-set update (Kim-Park)
@@ -559,16 +619,18 @@ __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_bo
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
   if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(as_kernel_f32, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(as_kernel_f32, dim3(g), dim3(64), lds, st, a);
   else
-    hipLaunchKernelGGL(as_kernel_f64, dim3(g), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(as_kernel_f64, dim3(g), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 // forward pass of the unconstrained small-chunk path from P2's row-major exports (ABT2, KR2)
 template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), 0, st, a);
+  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
+  hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 template hipError_t launch_fwd_rm<double>(const SplitArgs<double>&, hipStream_t);

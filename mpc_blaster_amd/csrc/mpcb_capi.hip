@@ -246,7 +246,7 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
-    // (+64: the 16-lane forward's 16-element row loads may read past the last ABT2 row)
+    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
     h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }

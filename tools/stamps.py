@@ -70,6 +70,15 @@ elif hasattr(lib, 'mpcb_debug_stamps_box') and w == 'c4':
     print(f'   forward tail per pass               {v[6] / its:9.0f}')
     print(f'   active-set update per iteration     {v[7] / its:9.0f}')
     print(f'   total                               {v[:8].sum():9.0f}')
+elif hasattr(lib, 'mpcb_debug_stamps_as') and w == 'c2':
+    ob = (ctypes.c_ulonglong * 12)()
+    lib.mpcb_debug_stamps_as.argtypes = [ctypes.c_void_p]
+    assert lib.mpcb_debug_stamps_as(ob) == 0
+    v = np.array(ob[:], dtype=np.float64) / N
+    print(f'{w}: 16-lane DPP forward (fwd_rm_kernel) cycles per stage (wave 0):')
+    for n, x in zip(['row assembly (+ slot wait)', 'du, outputs', 'row dot, refill issue'], v[4:7]):
+        print(f'   {n:36s} {x:9.0f}')
+    print(f'   {"total":36s} {v[4:7].sum():9.0f}')
 elif hasattr(lib, 'mpcb_debug_stamps_box'):
     ob = (ctypes.c_ulonglong * 12)()
     lib.mpcb_debug_stamps_box.argtypes = [ctypes.c_void_p]
