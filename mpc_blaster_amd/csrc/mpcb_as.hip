@@ -202,6 +202,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   int best = 0x7fffffff, pcount = 3;
   int n_fwd = 0, n_bst = 0;
   int kc = N - 1;               // highest stage whose active set changed (group-uniform)
+  bool u0fin = true;            // u0 of the flushed (final) pass is finite (staged outputs)
 #ifdef MPCB_STAMPS
   unsigned long long ast_prev = __builtin_amdgcn_s_memtime(), ast_acc[12] = {};
 #endif
@@ -257,7 +258,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         ne = nyb - (stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
         if (iterate) ngp = stl ? GP.at(k)[jx * SS] : T(0);
       };
-      bload(kmax);
+      // (a group loads only the stages it recomputes, k <= kc: the others' results are discarded)
+      if (kmax <= kc) bload(kmax);
       ASTAMP(0);
       for (int k = kmax; k >= 0; --k) {
         const bool act = k <= kc;   // this group's stage is recomputed
@@ -265,7 +267,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) col[i] = ncol[i];
         const T e = ne, yb = nyb, gpo = ngp;
-        if (k > 0) bload(k - 1);
+        if (k > 0 && k - 1 <= kc) bload(k - 1);
         // pt = p + P gap (component j), h = [A|B]^T pt
         T pt = pj;
         if (iterate) {
@@ -451,10 +453,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     auto gload = [&](int k) {
       if (BOX && (((lowm | upm) >> k) & 1ull)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
     };
+    // a converged group rides along with its wave's other groups: its loads are skipped and its
+    // results (garbage) neither written nor used
+    const bool fetch = !BOX || !done;
     static_for<FD>([&](auto s) {
-      if (decltype(s)::value < N) rload(decltype(s)::value, s);
+      if (decltype(s)::value < N && fetch) rload(decltype(s)::value, s);
     });
-    gload(0);
+    if (fetch) gload(0);
     auto stage = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
       const bool fixk = BOX && (((lowm | upm) >> k) & 1ull);   // input lanes: ju fixed at stage k
@@ -517,8 +522,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       } else {
         zj = v;
       }
-      if (k + FD < N) rload(k + FD, slot_tag);   // refill this slot FD stages ahead
-      if (k + 1 < N) gload(k + 1);
+      if (k + FD < N && fetch) rload(k + FD, slot_tag);   // refill this slot FD stages ahead
+      if (k + 1 < N && fetch) gload(k + 1);
       ASTAMP(6);
     };
     for (int k0 = 0; k0 < N; k0 += FD) {
@@ -526,29 +531,31 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         if (k0 + decltype(s)::value < N) stage(k0 + decltype(s)::value, s);
       });
     }
-    if (stage_out) {
-      if (stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
+    // outputs of this pass: staged rows leave as 16-B vectors once the pass is known to be final
+    // (the unconstrained pass; the active-set pass that converged or used the last iteration)
+    if (stage_out && stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
+    auto flush_out = [&]() {
       wave_lds_sync();
-      if (write) {   // the group's X block and U block are contiguous in the outputs
-        constexpr int V = 16 / sizeof(T);
-        typedef T Vec __attribute__((ext_vector_type(V)));
-        const int nx = (N + 1) * NX, nu = N * NU;
-        if (a.X) {
-          Vec* dst = reinterpret_cast<Vec*>(a.X + b * nx);
-          const Vec* src = reinterpret_cast<const Vec*>(xs);
-          for (int t = j; t < nx / V; t += NZ) dst[t] = src[t];
-        }
-        if (a.U) {
-          Vec* dst = reinterpret_cast<Vec*>(a.U + b * nu);
-          const Vec* src = reinterpret_cast<const Vec*>(us);
-          for (int t = j; t < nu / V; t += NZ) dst[t] = src[t];
-        }
-        if (!stl) a.u0[b * NU + ju] = us[ju];
+      constexpr int V = 16 / sizeof(T);
+      typedef T Vec __attribute__((ext_vector_type(V)));
+      const int nx = (N + 1) * NX, nu = N * NU;
+      if (a.X) {
+        Vec* dst = reinterpret_cast<Vec*>(a.X + b * nx);
+        const Vec* src = reinterpret_cast<const Vec*>(xs);
+        for (int t = j; t < nx / V; t += NZ) dst[t] = src[t];
       }
-      wave_lds_sync();
-    } else if (write && a.X && stl) {
-      a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
-    }
+      if (a.U) {
+        Vec* dst = reinterpret_cast<Vec*>(a.U + b * nu);
+        const Vec* src = reinterpret_cast<const Vec*>(us);
+        for (int t = j; t < nu / V; t += NZ) dst[t] = src[t];
+      }
+      if (!stl) a.u0[b * NU + ju] = us[ju];
+      u0fin = true;
+#pragma unroll
+      for (int m = 0; m < NU; ++m) u0fin = u0fin && (us[m] - us[m] == T(0));
+    };
+    if (!stage_out && write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+    if (!BOX && stage_out && write) flush_out();
     if constexpr (!BOX) break;
 
     // ------------------------------------------------ active-set update (Kim-Park)
@@ -582,6 +589,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     }
     // (the first masked pass is complete: P2 stored no snapshots)
     kc = changed ? (it == 0 ? N - 1 : 63 - __clzll(changed)) : -1;
+    if (BOX && stage_out && write && (gconv || it + 1 >= a.max_as_iter)) flush_out();
+    wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     if (!done && gconv) done = true;
     if (__all(done || !valid)) break;
     if (it + 1 >= a.max_as_iter) {
@@ -594,11 +603,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
 #endif
   if (valid && j == NX) {
-    T u0c[NU];
-    load_vec<NU>(a.u0 + b * NU, u0c);
-    bool fin = true;
+    bool fin = u0fin;
+    if (!(N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0)) {   // direct stores
+      T u0c[NU];
+      load_vec<NU>(a.u0 + b * NU, u0c);
 #pragma unroll
-    for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+      for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+    }
     // the QP status of the unconstrained pass (P2 wrote it) carries over
     const int32_t st0 = a.status[b];
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
