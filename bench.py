@@ -198,10 +198,10 @@ def phase_kernels(w):
     small = w['batch'] <= 16384
     names = {'nominal': f'nominal_quad_kernel<{t}>' if small else f'nominal_kernel<{t}>',
              'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}>'}
-    if w['box']:
-        names['forward'] = f'box_kernel_{w["dtype"]}<1>'
-    elif not w['hist']:
-        names['forward'] = f'box_kernel_{w["dtype"]}<2>' if small else f'forward_kernel<{t}, false>'
+    if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
+        names['forward'] = f'as_kernel_{w["dtype"]}'
+    elif not w['hist']:   # small chunks: the DPP forward pass over P2's row-major exports
+        names['forward'] = f'fwd_rm_kernel<{t}>' if small else f'forward_kernel<{t}, false>'
     return names
 
 

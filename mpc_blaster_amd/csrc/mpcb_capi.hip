@@ -65,6 +65,7 @@ struct mpcb_handle {
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
   int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
+  int q17 = 1;            // 17/6: the 16-lane DPP Riccati / interior-point kernel (MPCB_R17=0: riccati17_kernel)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -208,6 +209,7 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     if (chunk > max_batch) chunk = max_batch;
     h->full = 1;
     h->split = 1;
+    if (const char* e = getenv("MPCB_R17")) h->q17 = atoi(e) != 0;
     h->chunk = chunk;
     h->chunk_elems = full17_elems(cfg->N) * chunk;
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
@@ -352,6 +354,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.box = h->cfg.box_u;
     a.sbox = h->cfg.box_x;
     a.max_as_iter = h->cfg.max_as_iter;
+    a.q17 = h->q17;
     int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       a.b0 = b0;

@@ -16,6 +16,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "mpcb_common.h"
 #include "mpcb_model.h"
 
 namespace mpcb {
@@ -213,6 +214,7 @@ struct FullArgs {
   int box;           // input box lbu <= u <= ubu (interior-point iterations)
   int sbox;          // with box: state box lbx <= x_k <= ubx on stages 1..N-1
   int max_as_iter;   // iteration cap
+  int q17;           // the 16-lane DPP Riccati / interior-point kernel (mpcb_r17.hip); 0: riccati17_kernel
 };
 
 __host__ __device__ constexpr int64_t full17_elems(int N) {
@@ -222,8 +224,81 @@ __host__ __device__ constexpr int64_t full17_elems(int N) {
          2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17) + 4 * (int64_t)(N + 1) * NX17;
 }
 
+// n x n Cholesky (row-major H, lower L with 1/L_ii on the diagonal) and the solve L L^T x = b
+template <class T, int n>
+__device__ __forceinline__ void chol_n(const T* __restrict__ H, T* __restrict__ L) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      T acc = H[i * n + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) acc -= L[i * n + k] * L[j * n + k];
+      if (i == j) L[i * n + i] = inv_sqrt(acc);
+      else L[i * n + j] = acc * L[j * n + j];
+    }
+  }
+}
+template <class T, int n>
+__device__ __forceinline__ void chol_n_solve(const T* __restrict__ L, const T* __restrict__ b,
+                                             T* __restrict__ x) {
+  T y[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    T acc = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) acc -= L[i * n + k] * y[k];
+    y[i] = acc * L[i * n + i];
+  }
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i) {
+    T acc = y[i];
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) acc -= L[k * n + i] * x[k];
+    x[i] = acc * L[i * n + i];
+  }
+}
+
+// x[i] for a lane-dependent i < 17 without dynamic register indexing
+template <class T> __device__ __forceinline__ T sel17(const T* x, int i) {
+  const T lo = sel<16>(x, i & 15);
+  return (i == 16) ? x[16] : lo;
+}
+
+// Per-instance workspace carve (FullArgs::ws, full17_elems(N) elements per instance).
+template <class T>
+struct Ws17 {
+  T *XB, *UB, *AB, *KR, *GP;
+  T *DX, *DDX, *IP, *DDU, *IX;
+  static constexpr int KR_N = NU17 * NX17 + NU17;
+  __device__ __forceinline__ Ws17(T* ws, int N) {
+    XB = ws;                                     // [N+1][17] nominal states
+    UB = XB + (int64_t)(N + 1) * NX17;           // [N][6]    nominal inputs
+    AB = UB + (int64_t)N * NU17;                 // [N][23][17] column j of [A_k|B_k] at j*17
+    KR = AB + (int64_t)N * NZ17 * NX17;          // [N][6*17 + 6]: K[m][i] at i*6 + m, then k
+    GP = KR + (int64_t)N * KR_N;                 // [N][17] gaps
+    // input box (interior point): iterate dx, step, (du, lambda_l, lambda_u), step du
+    DX = GP + (int64_t)N * NX17;                 // [N+1][17]
+    DDX = DX + (int64_t)(N + 1) * NX17;          // [N+1][17]
+    IP = DDX + (int64_t)(N + 1) * NX17;          // [N][18]: du | lambda_l | lambda_u
+    DDU = IP + (int64_t)N * 18;                  // [N][6]
+    // state box: slacks and multipliers s_l | s_u | lambda_l | lambda_u of the rows of stage k
+    IX = DDU + (int64_t)N * NU17;                // [N+1][4][17]
+  }
+};
+
+constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
+constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
+constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
+constexpr int IPM17_SHORT_RUN = 10;
+// fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit
+// long before 1e-12), so the tolerances scale with the precision; the result is checked
+// against the fp64 oracle in tests/test_gpu_full17.py
+constexpr double IPM17_TOL_F32 = 1e-6, IPM17_BREAK_F32 = 1e-3, IPM17_RES_F32 = 1e-5;
+
 // ev (nullable): 4 events recorded before nominal17, after it, after lin17ws and after riccati17.
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev = nullptr);
+template <class T> hipError_t launch_riccati17q(const FullArgs<T>& a, hipStream_t st);
 template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
                               int64_t p_kb, const T* xbar, const T* ubar, T* A, T* Bm, T* xnext, hipStream_t st);

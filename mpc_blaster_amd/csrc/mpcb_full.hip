@@ -38,69 +38,6 @@ struct FullLds {
   T gp[NX17];         // gap of this stage
 };
 
-// n x n Cholesky (row-major H, lower L with 1/L_ii on the diagonal) and the solve L L^T x = b
-template <class T, int n>
-__device__ __forceinline__ void chol_n(const T* __restrict__ H, T* __restrict__ L) {
-#pragma unroll
-  for (int i = 0; i < n; ++i) {
-#pragma unroll
-    for (int j = 0; j <= i; ++j) {
-      T acc = H[i * n + j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) acc -= L[i * n + k] * L[j * n + k];
-      if (i == j) L[i * n + i] = inv_sqrt(acc);
-      else L[i * n + j] = acc * L[j * n + j];
-    }
-  }
-}
-template <class T, int n>
-__device__ __forceinline__ void chol_n_solve(const T* __restrict__ L, const T* __restrict__ b,
-                                             T* __restrict__ x) {
-  T y[n];
-#pragma unroll
-  for (int i = 0; i < n; ++i) {
-    T acc = b[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) acc -= L[i * n + k] * y[k];
-    y[i] = acc * L[i * n + i];
-  }
-#pragma unroll
-  for (int i = n - 1; i >= 0; --i) {
-    T acc = y[i];
-#pragma unroll
-    for (int k = i + 1; k < n; ++k) acc -= L[k * n + i] * x[k];
-    x[i] = acc * L[i * n + i];
-  }
-}
-
-// x[i] for a lane-dependent i < 17 without dynamic register indexing
-template <class T> __device__ __forceinline__ T sel17(const T* x, int i) {
-  const T lo = sel<16>(x, i & 15);
-  return (i == 16) ? x[16] : lo;
-}
-
-// Per-instance workspace carve (FullArgs::ws, full17_elems(N) elements per instance).
-template <class T>
-struct Ws17 {
-  T *XB, *UB, *AB, *KR, *GP;
-  T *DX, *DDX, *IP, *DDU, *IX;
-  static constexpr int KR_N = NU17 * NX17 + NU17;
-  __device__ __forceinline__ Ws17(T* ws, int N) {
-    XB = ws;                                     // [N+1][17] nominal states
-    UB = XB + (int64_t)(N + 1) * NX17;           // [N][6]    nominal inputs
-    AB = UB + (int64_t)N * NU17;                 // [N][23][17] column j of [A_k|B_k] at j*17
-    KR = AB + (int64_t)N * NZ17 * NX17;          // [N][6*17 + 6]: K[m][i] at i*6 + m, then k
-    GP = KR + (int64_t)N * KR_N;                 // [N][17] gaps
-    // input box (interior point): iterate dx, step, (du, lambda_l, lambda_u), step du
-    DX = GP + (int64_t)N * NX17;                 // [N+1][17]
-    DDX = DX + (int64_t)(N + 1) * NX17;          // [N+1][17]
-    IP = DDX + (int64_t)(N + 1) * NX17;          // [N][18]: du | lambda_l | lambda_u
-    DDU = IP + (int64_t)N * 18;                  // [N][6]
-    // state box: slacks and multipliers s_l | s_u | lambda_l | lambda_u of the rows of stage k
-    IX = DDU + (int64_t)N * NU17;                // [N+1][4][17]
-  }
-};
-
 // ---- phase 0: nominal trajectory, one thread per instance (a serial RK4 chain) ---------------
 template <class T>
 __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
@@ -550,15 +487,6 @@ __device__ __forceinline__ bool forward17(const R17<T>& r, T dxj, bool write) {
   return fin;
 }
 
-constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
-constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-8, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
-constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
-constexpr int IPM17_SHORT_RUN = 10;
-// fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit
-// long before 1e-12), so the tolerances scale with the precision; the result is checked
-// against the fp64 oracle in tests/test_gpu_full17.py
-constexpr double IPM17_TOL_F32 = 1e-6, IPM17_BREAK_F32 = 1e-3, IPM17_RES_F32 = 1e-5;
-
 // BOX: the input box lbu <= u <= ubu of the reference OCP (blastermodel.py:259-264; thrust
 // [0, 65] N, swivel rate +-0.0873 rad/s) by a primal-dual interior point over the Riccati
 // recursion (acados uses HPIPM's; oracle.ocp.ipm_box_solve is the same iteration, incl. the
@@ -831,10 +759,14 @@ template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + GQ17 - 1) / GQ17)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
-  if (a.box)
+  if (a.q17) {
+    const hipError_t e = launch_riccati17q<T>(a, st);
+    if (e != hipSuccess) return e;
+  } else if (a.box) {
     hipLaunchKernelGGL((riccati17_kernel<T, true>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((riccati17_kernel<T, false>), dim3((unsigned)((a.nb + G17 - 1) / G17)), dim3(64), 0, st, a);
+  }
   if (ev) (void)hipEventRecord(ev[3], st);
   return hipGetLastError();
 }

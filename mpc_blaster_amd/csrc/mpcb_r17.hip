@@ -1,0 +1,797 @@
+// mpcb_r17.hip — the 17/6 Riccati pass and its interior point in a 16-lane DPP layout
+// (blastermodel.py:214-292, acados_ocp_blasterModel.json: N = 60, nx = 17,
+// nu = 6).  Same arithmetic as riccati17_kernel (mpcb_full.hip), which stays as the reference
+// implementation behind MPCB_R17=0; this kernel is the default.
+//
+// Layout.  Four instances per wavefront, 16 lanes each (one DPP row per instance), so every
+// operand exchange inside an instance is a row broadcast folded into the consuming FMA
+// (v_fmac_f{32,64}_dpp ... row_newbcast:L) — no LDS operands in the products.  The 23 columns of
+// [A|B] do not fit 16 lanes, but 9 of them are structural (f17 does not depend on the position
+// or POC states and is linear in the velocity, mpcb_full.hip lin17ws):
+//   identity columns  AB[:, c] = e_c                 c in {0,1,2, 14,15,16}
+//   shear columns     AB[:, 6+c] = e_{6+c} + h e_c + h Jp[:, c] e_poc
+// Lane t holds column z(t) of [A|B]: the 14 dense columns (Euler angles 3-5, body rates 9-11,
+// swivel angles 12-13, inputs 17-22) and the shear columns 6, 7; the third shear column (8) is
+// implicit (its five nonzeros are read from the cached [A|B]).  Lane t also owns column s(t) of
+// the value-function Hessian P: s = z for the state-column lanes 0-7, 14, 15, and the identity
+// states 0,1,2,14,15,16 for the input lanes 8-13.  P's 17th column (state 8) is never held as an
+// array: by symmetry it is the set of entries P[8, s(t)] across the lanes, plus P[8,8].
+//
+// Per stage (backward), for the four instances of a wave:
+//   Y = P [A|B]_z          16 row-broadcast passes of a P column (+ the distributed column 8)
+//   G_z = [A|B]^T Y_z      16 row-broadcast passes of [A|B] columns; identity rows are Y rows
+//   Huu, h_u               input lanes' columns through a small LDS block
+//   G for identity states  rows gathered from the other lanes' Y (LDS), the rest from P
+//   K, k                   6x6 Cholesky per lane (redundant), own column of K
+//   P_new = G + Hxu K      6 row-broadcast passes, then the symmetric exchange (LDS)
+// Dense flop count per stage (tools/bench_full17.py): 39,316; the structural columns make the
+// executed count about 60 % of that.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcb.h"
+#include "mpcb_common.h"
+#include "mpcb_full.h"
+
+namespace mpcb {
+namespace q17 {
+
+constexpr int LN = 16, GR = 64 / LN;   // lanes per instance, instances per wavefront
+constexpr int OM = 8;                  // the state whose P column is held distributed
+
+// lane t -> z column of [A|B] it holds, state column of P it owns; state i -> owning lane
+__host__ __device__ constexpr int zcol(int t) { return t < 3 ? 3 + t : t < 8 ? 6 + t : t < 14 ? 9 + t : t - 8; }
+__host__ __device__ constexpr int sown(int t) { return t < 8 ? zcol(t) : t < 11 ? t - 8 : t < 14 ? t + 3 : t - 8; }
+__host__ __device__ constexpr int tstate(int i) {
+  return i < 3 ? 8 + i : i < 6 ? i - 3 : i < 8 ? i + 8 : i == 8 ? -1 : i < 14 ? i - 6 : i - 3;
+}
+// identity states held by the input lanes, in lane order (lane 8 + ci owns IDS[ci])
+__host__ __device__ constexpr int ids(int ci) { return ci < 3 ? ci : ci + 11; }
+// nonzero rows of the implicit shear column 8: AB[8,8] = 1, AB[2,8] = h, AB[14+m,8] = h Jp[m][2]
+__host__ __device__ constexpr int c8row(int r) { return r == 0 ? 8 : r == 1 ? 2 : 12 + r; }
+
+// ---- row-broadcast FMAs ----------------------------------------------------------------------
+// The leading s_nop covers the VALU-write -> DPP-read wait states the hazard recognizer does not
+// insert for inline asm (no DPP source is written inside a block); see mpcb_split.h.
+#define Q17_BC(op, d, s, b, l) op " %" #d ", %" #s ", %" #b " row_newbcast:" l " row_mask:0xf bank_mask:0xf\n\t"
+
+// y[i] += bcast_L(a[i]) * b (i < 17), h += bcast_L(ah) * b
+#define Q17_BC18(OP)                                                                                        \
+  asm("s_nop 4\n\t" Q17_BC(OP, 0, 18, 36, "%c37") Q17_BC(OP, 1, 19, 36, "%c37") Q17_BC(OP, 2, 20, 36, "%c37") \
+      Q17_BC(OP, 3, 21, 36, "%c37") Q17_BC(OP, 4, 22, 36, "%c37") Q17_BC(OP, 5, 23, 36, "%c37")               \
+      Q17_BC(OP, 6, 24, 36, "%c37") Q17_BC(OP, 7, 25, 36, "%c37") Q17_BC(OP, 8, 26, 36, "%c37")               \
+      Q17_BC(OP, 9, 27, 36, "%c37") Q17_BC(OP, 10, 28, 36, "%c37") Q17_BC(OP, 11, 29, 36, "%c37")             \
+      Q17_BC(OP, 12, 30, 36, "%c37") Q17_BC(OP, 13, 31, 36, "%c37") Q17_BC(OP, 14, 32, 36, "%c37")            \
+      Q17_BC(OP, 15, 33, 36, "%c37") Q17_BC(OP, 16, 34, 36, "%c37") Q17_BC(OP, 17, 35, 36, "%c37")            \
+      : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]),       \
+        "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]), "+v"(y[12]), "+v"(y[13]), "+v"(y[14]),              \
+        "+v"(y[15]), "+v"(y[16]), "+v"(h)                                                                     \
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),  \
+        "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]), "v"(a[16]),       \
+        "v"(ah), "v"(b), "i"(L))
+template <int L, class T>
+__device__ __forceinline__ void bc18(T (&y)[NX17], T& h, const T (&a)[NX17], T ah, T b) {
+  if constexpr (sizeof(T) == 8) Q17_BC18("v_fmac_f64_dpp"); else Q17_BC18("v_fmac_f32_dpp");
+}
+
+// acc_t += bcast_t(a) * b for the 16 lanes t of the row; acc_t = g[t] (DIAG) or y[sown(t)]
+#define Q17_D16(OP, ...)                                                                                  \
+  asm("s_nop 4\n\t" Q17_BC(OP, 0, 16, 17, "0") Q17_BC(OP, 1, 16, 17, "1") Q17_BC(OP, 2, 16, 17, "2")      \
+      Q17_BC(OP, 3, 16, 17, "3") Q17_BC(OP, 4, 16, 17, "4") Q17_BC(OP, 5, 16, 17, "5")                    \
+      Q17_BC(OP, 6, 16, 17, "6") Q17_BC(OP, 7, 16, 17, "7") Q17_BC(OP, 8, 16, 17, "8")                    \
+      Q17_BC(OP, 9, 16, 17, "9") Q17_BC(OP, 10, 16, 17, "10") Q17_BC(OP, 11, 16, 17, "11")                \
+      Q17_BC(OP, 12, 16, 17, "12") Q17_BC(OP, 13, 16, 17, "13") Q17_BC(OP, 14, 16, 17, "14")              \
+      Q17_BC(OP, 15, 16, 17, "15")                                                                        \
+      : __VA_ARGS__                                                                                       \
+      : "v"(a), "v"(b))
+#define Q17_G16 "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]), \
+    "+v"(g[7]), "+v"(g[8]), "+v"(g[9]), "+v"(g[10]), "+v"(g[11]), "+v"(g[12]), "+v"(g[13]),         \
+    "+v"(g[14]), "+v"(g[15])
+#define Q17_YS16 "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]), "+v"(y[12]), \
+    "+v"(y[13]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[14]), "+v"(y[15]), "+v"(y[16]),            \
+    "+v"(y[6]), "+v"(y[7])
+template <class T> __device__ __forceinline__ void diag16(T (&g)[LN], T a, T b) {
+  if constexpr (sizeof(T) == 8) Q17_D16("v_fmac_f64_dpp", Q17_G16); else Q17_D16("v_fmac_f32_dpp", Q17_G16);
+}
+template <class T> __device__ __forceinline__ void diag16_sown(T (&y)[NX17], T a, T b) {
+  static_assert(sown(0) == 3 && sown(8) == 0 && sown(11) == 14 && sown(14) == 6, "Q17_YS16 order");
+  if constexpr (sizeof(T) == 8) Q17_D16("v_fmac_f64_dpp", Q17_YS16); else Q17_D16("v_fmac_f32_dpp", Q17_YS16);
+}
+
+// acc += bcast_t(a) * w[t] for the 16 lanes t of the row (one dependent chain)
+#define Q17_C16(OP)                                                                                      \
+  asm("s_nop 4\n\t" Q17_BC(OP, 0, 1, 2, "0") Q17_BC(OP, 0, 1, 3, "1") Q17_BC(OP, 0, 1, 4, "2")           \
+      Q17_BC(OP, 0, 1, 5, "3") Q17_BC(OP, 0, 1, 6, "4") Q17_BC(OP, 0, 1, 7, "5") Q17_BC(OP, 0, 1, 8, "6") \
+      Q17_BC(OP, 0, 1, 9, "7") Q17_BC(OP, 0, 1, 10, "8") Q17_BC(OP, 0, 1, 11, "9")                       \
+      Q17_BC(OP, 0, 1, 12, "10") Q17_BC(OP, 0, 1, 13, "11") Q17_BC(OP, 0, 1, 14, "12")                   \
+      Q17_BC(OP, 0, 1, 15, "13") Q17_BC(OP, 0, 1, 16, "14") Q17_BC(OP, 0, 1, 17, "15")                   \
+      : "+v"(acc)                                                                                        \
+      : "v"(a), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]),  \
+        "v"(w[8]), "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]))
+template <class T> __device__ __forceinline__ void chain16(T& acc, T a, const T (&w)[LN]) {
+  if constexpr (sizeof(T) == 8) Q17_C16("v_fmac_f64_dpp"); else Q17_C16("v_fmac_f32_dpp");
+}
+
+// lane L's v in every lane of the row (0 + bcast_L(v) * 1: exact)
+template <int L, class T> __device__ __forceinline__ T bcast(T v) {
+  T r = T(0);
+  const T one = T(1);
+  if constexpr (sizeof(T) == 8)
+    asm("s_nop 4\n\t" Q17_BC("v_fmac_f64_dpp", 0, 1, 2, "%c3") : "+v"(r) : "v"(v), "v"(one), "i"(L));
+  else
+    asm("s_nop 4\n\t" Q17_BC("v_fmac_f32_dpp", 0, 1, 2, "%c3") : "+v"(r) : "v"(v), "v"(one), "i"(L));
+  return r;
+}
+#undef Q17_BC18
+#undef Q17_D16
+#undef Q17_C16
+
+// sum / min / max over the 16 lanes of the row (DPP broadcasts of every lane: 16 instructions)
+template <class T> __device__ __forceinline__ T row_sum(T v) {
+  T s = T(0);
+  static_for<LN>([&](auto l) { s += bcast<decltype(l)::value>(v); });
+  return s;
+}
+template <class T> __device__ __forceinline__ T row_min(T v) {
+  T s = v;
+  static_for<LN>([&](auto l) { s = fmin(s, bcast<decltype(l)::value>(v)); });
+  return s;
+}
+template <class T> __device__ __forceinline__ T row_max(T v) {
+  T s = v;
+  static_for<LN>([&](auto l) { s = fmax(s, bcast<decltype(l)::value>(v)); });
+  return s;
+}
+__device__ __forceinline__ int row_or(int v) {
+  const float f = row_max((float)v);
+  return f > 0.f ? 1 : 0;
+}
+
+// per-instance LDS block
+template <class T> struct Lds {
+  T V[24];            // cost residual (ybar + iterate - yref) by z index
+  T HU[NU17][8];      // input lane m: G[17+n, 17+m] (n < 6), h_u[m], G[8, 17+m]
+  T YC[6][17];        // lane t: Y[c, z(t)] for the identity states c = ids(0..5) (stride 17: banks)
+  T X[LN][NX17];      // P_new columns (symmetric exchange)
+};
+
+template <class T>
+struct Ctx {
+  const FullArgs<T>& a;
+  Ws17<T> w;
+  const T* xr;
+  const T* ur;
+  Lds<T>& L;
+  const T* sQ;        // s * Q (row-major 17 x 17), LDS
+  const T* sR;        // s * R (6 x 6), LDS
+  int t, s, z, m;     // lane in the row, owned state, z column, input index (input lanes; else 0)
+  bool in, valid;
+};
+
+// state-box row (k, i): dx-coordinate bounds, the iterate and its slacks / multipliers
+template <class T>
+struct SRow {
+  T y, lb, ub, sl, su, ll, lu, rl, ru;
+  __device__ __forceinline__ SRow(T y_, T xb, T lbx, T ubx, T sl_, T su_, T ll_, T lu_)
+      : y(y_), lb(lbx - xb), ub(ubx - xb), sl(sl_), su(su_), ll(ll_), lu(lu_) {
+    rl = y - lb - sl;
+    ru = ub - y - su;
+  }
+  __device__ __forceinline__ SRow(const Ctx<T>& r, int k, int i)
+      : SRow(r.w.DX[(int64_t)k * NX17 + i], r.w.XB[(int64_t)k * NX17 + i], r.a.W->lbx[i], r.a.W->ubx[i],
+             r.w.IX[(int64_t)k * 4 * NX17 + i], r.w.IX[(int64_t)k * 4 * NX17 + NX17 + i],
+             r.w.IX[(int64_t)k * 4 * NX17 + 2 * NX17 + i], r.w.IX[(int64_t)k * 4 * NX17 + 3 * NX17 + i]) {}
+  __device__ __forceinline__ void barrier(T smu, T& D, T& d) const {
+    D = ll / sl + lu / su;
+    d = -smu * (T(1) / sl - T(1) / su) + (ll / sl) * rl - (lu / su) * ru;
+  }
+};
+
+// Stage data loaded one stage ahead, as raw loads: every value is consumed a stage later (any
+// arithmetic or select on a load here would wait for it on the spot).  The interior point's
+// iterate, multipliers and state-row slacks are loaded unconditionally (the workspace always holds
+// them; unused values are discarded by selects, never multiplied).
+template <class T>
+struct Pre {
+  T ab[NX17];      // column z of [A_k | B_k]
+  T a8[5];         // the nonzeros of the implicit column 8 (rows c8row(0..4))
+  T xs, x8, xrs, xr8, ub, urm;          // xbar_k[s], xbar_k[8], xref_k[s], xref_k[8], ubar_k[m], uref_k[m]
+  T dxs, dx8, du, ll, lu;               // interior point: dx_k[s], dx_k[8], (du, lambda_l, lambda_u)_k[m]
+  T ixs[4], ix8[4];                     // state rows (s_l, s_u, lambda_l, lambda_u) of s and 8
+};
+
+template <class T>
+__device__ __forceinline__ void prefetch(const Ctx<T>& r, int k, Pre<T>& p) {
+  const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) p.ab[i] = ABk[r.z * NX17 + i];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) p.a8[q] = ABk[OM * NX17 + c8row(q)];
+  const int64_t kx = (int64_t)k * NX17;
+  p.xs = r.w.XB[kx + r.s];
+  p.x8 = r.w.XB[kx + OM];
+  p.xrs = r.xr[kx + r.s];
+  p.xr8 = r.xr[kx + OM];
+  p.ub = r.w.UB[(int64_t)k * NU17 + r.m];
+  p.urm = r.ur[(int64_t)k * NU17 + r.m];
+  p.dxs = r.w.DX[kx + r.s];
+  p.dx8 = r.w.DX[kx + OM];
+  const T* ip = r.w.IP + (int64_t)k * 18;
+  p.du = ip[r.m];
+  p.ll = ip[6 + r.m];
+  p.lu = ip[12 + r.m];
+  const T* ix = r.w.IX + (int64_t)k * 4 * NX17;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    p.ixs[e] = ix[e * NX17 + r.s];
+    p.ix8[e] = ix[e * NX17 + OM];
+  }
+}
+
+// Riccati backward over the cached [A|B] (+ gaps in iterate mode, + the interior point's barrier
+// terms and the iterate shift when r.a.box).  Writes K (row-major 6 x 17) and k to KR.
+template <class T>
+__device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
+  const FullArgs<T>& a = r.a;
+  const bool ipm = a.box != 0;
+  const bool gaps = !ipm && a.mode == MPCB_MODE_ITERATE;
+  const bool sbox = ipm && a.sbox != 0;
+  Lds<T>& L = r.L;
+  const int t = r.t, s = r.s, N = a.N;
+  const bool in = r.in;
+  const Weights17<T>& W = *a.W;
+  constexpr int KR_N = Ws17<T>::KR_N;
+  const uint64_t m_in = lane_mask(in);
+  // terminal cost: P_N = QN, p_N = QN (x_N - xref_N)
+  T Pc[NX17], P88, pj, p8;
+  {
+    T xs = r.w.XB[(int64_t)N * NX17 + s], x8 = r.w.XB[(int64_t)N * NX17 + OM];
+    if (ipm) {
+      xs += r.w.DX[(int64_t)N * NX17 + s];
+      x8 += r.w.DX[(int64_t)N * NX17 + OM];
+    }
+    L.V[s] = xs - r.xr[(int64_t)N * NX17 + s];
+    L.V[OM] = x8 - r.xr[(int64_t)N * NX17 + OM];
+    wave_lds_sync();
+    pj = T(0);
+    p8 = T(0);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      const T vi = L.V[i];
+      pj += W.QN[s * NX17 + i] * vi;
+      p8 += W.QN[OM * NX17 + i] * vi;
+      Pc[i] = W.QN[i * NX17 + s];
+    }
+    P88 = W.QN[OM * NX17 + OM];
+    wave_lds_sync();
+  }
+  // box constants in registers (a load consumed on the spot would wait inside the stage loop)
+  const T lbm = W.lbu[r.m], ubm = W.ubu[r.m];
+  const T lbs = W.lbx[s], ubs = W.ubx[s], lb8 = W.lbx[OM], ub8 = W.ubx[OM];
+  bool qp_ok = true;
+  Pre<T> nx;
+  prefetch(r, N - 1, nx);
+  for (int k = N - 1; k >= 0; --k) {
+    const Pre<T> cu = nx;
+    prefetch(r, k > 0 ? k - 1 : 0, nx);   // (unconditional: no branch join on the loads)
+    // cost residual into LDS (general Q, R); pt = p + P gap (iterate mode)
+    L.V[s] = (ipm ? cu.xs + cu.dxs : cu.xs) - cu.xrs;
+    L.V[OM] = (ipm ? cu.x8 + cu.dx8 : cu.x8) - cu.xr8;
+    if (in) L.V[NX17 + r.m] = (ipm ? cu.ub + cu.du : cu.ub) - cu.urm;
+    T pt = pj, pt8 = p8;
+    if (gaps) {
+      const T* gk = r.w.GP + (int64_t)k * NX17;
+      T prow = Pc[OM] * gk[s];   // P[8, s] gap[s]: summed over the row below
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) pt += Pc[i] * gk[i];
+      pt8 += P88 * gk[OM] + row_sum(prow);
+    }
+    // ---- Y = P [A|B]_z and h_AB = [A|B]_z^T pt
+    T y[NX17], hab = T(0);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) y[i] = T(0);
+    static_for<LN>([&](auto l) {
+      constexpr int tl = decltype(l)::value;
+      bc18<tl>(y, hab, Pc, pt, cu.ab[sown(tl)]);
+    });
+    diag16_sown(y, Pc[OM], cu.ab[OM]);
+    y[OM] += P88 * cu.ab[OM];
+    hab += pt8 * cu.ab[OM];
+    // ---- G_z = [A|B]^T Y_z: rows z(t') by row broadcasts of [A|B] columns, identity rows = Y rows,
+    // row 8 by the shear column
+    T g[LN];
+#pragma unroll
+    for (int i = 0; i < LN; ++i) g[i] = T(0);
+#pragma unroll
+    for (int l = 0; l < NX17; ++l) diag16(g, cu.ab[l], y[l]);
+    T g8 = T(0);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) g8 += cu.a8[q] * y[c8row(q)];
+    // identity rows of this lane's Y for the identity-state lanes (their G column, by symmetry)
+#pragma unroll
+    for (int ci = 0; ci < 6; ++ci) L.YC[ci][t] = y[ids(ci)];
+    wave_lds_sync();
+    // ---- input lanes: their column G[:, 17+m] (+ s R, + barrier) -> Huu, h_u, Hux[:, 8]
+    if (in) {
+      const int m = r.m;
+      T hu = hab;
+#pragma unroll
+      for (int n = 0; n < NU17; ++n) {
+        const T wr = r.sR[n * NU17 + m];
+        hu += wr * L.V[NX17 + n];
+        L.HU[m][n] = g[8 + n] + wr;
+      }
+      if (ipm) {
+        const T sl = cu.du - (lbm - cu.ub), su = (ubm - cu.ub) - cu.du;
+        L.HU[m][m] += cu.ll / sl + cu.lu / su;
+        hu -= smu * (T(1) / sl - T(1) / su);
+      }
+      L.HU[m][6] = hu;
+      L.HU[m][7] = g8;
+    }
+    wave_lds_sync();
+    // ---- this lane's state column Gs = G[:, s] (23 rows by z index) and gradient h_s
+    T Gs[NZ17];
+    {
+      // column lanes: (g, Y rows, g8); identity lanes: rows z(t') from the lanes' Y (YC), identity
+      // rows from P (AB[:, c] = e_c), row 8 by the shear column applied to P's column
+      const int ci = in ? r.m : 0;
+      T spc = T(0);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) spc += cu.a8[q] * Pc[c8row(q)];
+#pragma unroll
+      for (int tp = 0; tp < LN; ++tp) Gs[zcol(tp)] = csel(m_in, L.YC[ci][tp], g[tp]);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) Gs[ids(q)] = csel(m_in, Pc[ids(q)], y[ids(q)]);
+      Gs[OM] = csel(m_in, spc, g8);
+    }
+    T hs = in ? pt : hab;   // AB[:, c]^T pt = pt_c for an identity state
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      const T wq = r.sQ[i * NX17 + s];
+      Gs[i] += wq;
+      hs += wq * L.V[i];
+    }
+    // row 8 of every lane's G column is needed as the distributed column 8 of G; G[8,8] itself:
+    // a^T P a with a = AB[:, 8] (rows 8, 2, 14..16) from P88, the lanes' P[8, .] and (P a)
+    T spc_own = T(0);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) spc_own += cu.a8[q] * Pc[c8row(q)];   // (P a)_s
+    T pa8 = P88 * cu.a8[0];                                             // (P a)_8
+    T G88 = T(0), h8 = T(0);
+    {
+      const T pc8 = Pc[OM];
+      pa8 += bcast<tstate(2)>(pc8) * cu.a8[1] + bcast<tstate(14)>(pc8) * cu.a8[2] +
+             bcast<tstate(15)>(pc8) * cu.a8[3] + bcast<tstate(16)>(pc8) * cu.a8[4];
+      G88 = cu.a8[0] * pa8 + cu.a8[1] * bcast<tstate(2)>(spc_own) + cu.a8[2] * bcast<tstate(14)>(spc_own) +
+            cu.a8[3] * bcast<tstate(15)>(spc_own) + cu.a8[4] * bcast<tstate(16)>(spc_own);
+      h8 = cu.a8[0] * pt8 + cu.a8[1] * bcast<tstate(2)>(pt) + cu.a8[2] * bcast<tstate(14)>(pt) +
+           cu.a8[3] * bcast<tstate(15)>(pt) + cu.a8[4] * bcast<tstate(16)>(pt);
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) h8 += r.sQ[OM * NX17 + i] * L.V[i];
+      G88 += r.sQ[OM * NX17 + OM];
+    }
+    if (sbox && k > 0) {   // state-box rows of this stage: barrier terms on the state diagonals
+      T D, d;
+      SRow<T>(cu.dxs, cu.xs, lbs, ubs, cu.ixs[0], cu.ixs[1], cu.ixs[2], cu.ixs[3]).barrier(smu, D, d);
+#pragma unroll
+      for (int i = 0; i < NX17; ++i) Gs[i] += (i == s) ? D : T(0);
+      hs += d;
+      SRow<T>(cu.dx8, cu.x8, lb8, ub8, cu.ix8[0], cu.ix8[1], cu.ix8[2], cu.ix8[3]).barrier(smu, D, d);
+      G88 += D;
+      h8 += d;
+    }
+    // ---- Huu (lower triangle from the column owners), Cholesky, k, K columns
+    T H[NU17 * NU17], hu[NU17], hx8[NU17];
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) {
+#pragma unroll
+      for (int j = 0; j <= i; ++j) H[i * NU17 + j] = L.HU[j][i];
+      hu[i] = L.HU[i][6];
+      hx8[i] = L.HU[i][7];
+    }
+    T Lc[NU17 * NU17];
+    chol_n<T, NU17>(H, Lc);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) ok = ok && (Lc[i * NU17 + i] == Lc[i * NU17 + i]);
+    qp_ok = qp_ok && ok;
+    T kff[NU17], Ks[NU17], K8[NU17], nb[NU17];
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) nb[i] = -hu[i];
+    chol_n_solve<T, NU17>(Lc, nb, kff);
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) nb[i] = -Gs[NX17 + i];
+    chol_n_solve<T, NU17>(Lc, nb, Ks);
+#pragma unroll
+    for (int i = 0; i < NU17; ++i) nb[i] = -hx8[i];
+    chol_n_solve<T, NU17>(Lc, nb, K8);
+    if (r.valid) {   // KR: K row-major [6][17], then k[6]
+      T* kr = r.w.KR + (int64_t)k * KR_N;
+#pragma unroll
+      for (int i = 0; i < NU17; ++i) kr[i * NX17 + s] = Ks[i];
+      if (t == 0) {
+#pragma unroll
+        for (int i = 0; i < NU17; ++i) kr[i * NX17 + OM] = K8[i];
+      }
+      if (in) kr[NU17 * NX17 + r.m] = sel<NU17>(kff, r.m);
+    }
+    // ---- P_new[:, s] = G_xx[:, s] + Hxu K[:, s]; p_new; the 8 entries
+    T Pn[NX17];
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) Pn[i] = Gs[i];
+#pragma unroll
+    for (int n = 0; n < NU17; ++n) {
+      diag16_sown(Pn, Gs[NX17 + n], Ks[n]);
+      Pn[OM] += hx8[n] * Ks[n];
+    }
+    T pn = hs, pn8 = h8, P88n = G88;
+#pragma unroll
+    for (int n = 0; n < NU17; ++n) {
+      pn += Gs[NX17 + n] * kff[n];
+      pn8 += hx8[n] * kff[n];
+      P88n += hx8[n] * K8[n];
+    }
+#ifdef MPCB_Q17_DEBUG
+    if (blockIdx.x == 0 && threadIdx.x < LN && k >= N - 2) {
+      printf("QG %d %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", k, t, s, (double)Gs[0], (double)Gs[1], (double)Gs[2], (double)Gs[3], (double)Gs[4], (double)Gs[5], (double)Gs[6], (double)Gs[7], (double)Gs[8], (double)Gs[9], (double)Gs[10], (double)Gs[11], (double)Gs[12], (double)Gs[13], (double)Gs[14], (double)Gs[15], (double)Gs[16], (double)Gs[17], (double)Gs[18], (double)Gs[19], (double)Gs[20], (double)Gs[21], (double)Gs[22]);
+      printf("QH %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", k, t, (double)hs, (double)h8, (double)G88, (double)pt, (double)Ks[0], (double)Ks[1], (double)Ks[2], (double)Ks[3], (double)Ks[4], (double)Ks[5], (double)kff[0], (double)kff[1], (double)kff[2], (double)kff[3], (double)kff[4], (double)kff[5]);
+      printf("QP %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", k, t, (double)Pn[0], (double)Pn[1], (double)Pn[2], (double)Pn[3], (double)Pn[4], (double)Pn[5], (double)Pn[6], (double)Pn[7], (double)Pn[8], (double)Pn[9], (double)Pn[10], (double)Pn[11], (double)Pn[12], (double)Pn[13], (double)Pn[14], (double)Pn[15], (double)Pn[16]);
+      printf("QY %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", k, t, (double)y[0], (double)y[1], (double)y[2], (double)y[3], (double)y[4], (double)y[5], (double)y[6], (double)y[7], (double)y[8], (double)y[9], (double)y[10], (double)y[11], (double)y[12], (double)y[13], (double)y[14], (double)y[15], (double)y[16]);
+    }
+#endif
+    // symmetric by construction: entry (i, s) from the lane max(own, owner of i)
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) L.X[t][i] = Pn[i];
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      if (i == OM) {
+        Pc[i] = Pn[i];
+      } else {
+        const T o = L.X[tstate(i)][s];
+        Pc[i] = csel(lane_mask(tstate(i) > t), o, Pn[i]);
+      }
+    }
+    P88 = P88n;
+    pj = pn;
+    p8 = pn8;
+    wave_lds_sync();
+  }
+  return qp_ok;
+}
+
+// Forward pass over K, k.  GAIN: du = K dx + k; else du from the interior point's iterate (the
+// starting trajectory).  STEP: the Newton step (zero gaps, dx_0 = 0) into DDX / DDU; !STEP and
+// !OUT: the iterate into DX.  OUT: X = xbar + dx, U = ubar + du, u0 (when write).  Returns this
+// lane's finiteness.
+template <class T, bool GAIN, bool STEP, bool OUT>
+__device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool write) {
+  const FullArgs<T>& a = r.a;
+  const int t = r.t, s = r.s, N = a.N;
+  const bool in = r.in;
+  constexpr int KR_N = Ws17<T>::KR_N;
+  const bool gaps = !STEP && a.mode == MPCB_MODE_ITERATE;   // (the starting trajectory of the interior point too)
+  const int64_t b = a.b0 + (r.w.XB - a.ws) / full17_elems(N);
+  const uint64_t m_in = lane_mask(in), m_id = m_in;   // identity-state lanes = input lanes
+  bool fin = true;
+  // stage rows one stage ahead: K row m and k_m (input lanes), row s and row 8 of [A|B]
+  struct Row { T kr[LN], k8, kf, du, ab[LN], ab8[LN], c8s, c88, gs, g8; };
+  auto load = [&](int k, Row& o) {
+    const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
+    if constexpr (GAIN) {
+      const T* Kk = r.w.KR + (int64_t)k * KR_N;
+#pragma unroll
+      for (int tp = 0; tp < LN; ++tp) o.kr[tp] = Kk[r.m * NX17 + sown(tp)];
+      o.k8 = Kk[r.m * NX17 + OM];
+      o.kf = Kk[NU17 * NX17 + r.m];
+    } else {
+      o.du = r.w.IP[(int64_t)k * 18 + r.m];
+    }
+#pragma unroll
+    for (int tp = 0; tp < LN; ++tp) {
+      o.ab[tp] = ABk[zcol(tp) * NX17 + s];
+      o.ab8[tp] = ABk[zcol(tp) * NX17 + OM];
+    }
+    o.c8s = ABk[OM * NX17 + s];
+    o.c88 = ABk[OM * NX17 + OM];
+    o.gs = r.w.GP[(int64_t)k * NX17 + s];   // (raw: selected at use)
+    o.g8 = r.w.GP[(int64_t)k * NX17 + OM];
+  };
+  Row nr;
+  load(0, nr);
+  for (int k = 0; k < N; ++k) {
+    const Row cr = nr;
+    if (k + 1 < N) load(k + 1, nr);
+    T du;
+    if constexpr (GAIN) {
+      du = cr.kf + cr.k8 * dx8;
+      chain16(du, dxs, cr.kr);
+    } else {
+      du = cr.du;
+    }
+    if (!in) du = T(0);
+    if (STEP && r.valid) {
+      r.w.DDX[(int64_t)k * NX17 + s] = dxs;
+      if (t == 0) r.w.DDX[(int64_t)k * NX17 + OM] = dx8;
+      if (in) r.w.DDU[(int64_t)k * NU17 + r.m] = du;
+    }
+    if (!STEP && !OUT && r.valid) {
+      r.w.DX[(int64_t)k * NX17 + s] = dxs;
+      if (t == 0) r.w.DX[(int64_t)k * NX17 + OM] = dx8;
+    }
+    if (OUT && write && a.X) {
+      T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
+      xo[s] = r.w.XB[(int64_t)k * NX17 + s] + dxs;
+      if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + dx8;
+    }
+    if (in) {
+      const T uo = r.w.UB[(int64_t)k * NU17 + r.m] + du;
+      fin = fin && ((uo - uo) == T(0));
+      if (OUT && write && a.U) a.U[(b * (int64_t)N + k) * NU17 + r.m] = uo;
+      if (OUT && write && k == 0) a.u0[b * NU17 + r.m] = uo;
+    }
+    // dx' = [A|B] (dx, du) + gap: lanes broadcast their z value (du on input lanes)
+    const T zb = csel(m_in, du, dxs);
+    T acc = (gaps ? cr.gs : T(0)) + cr.c8s * dx8 + csel(m_id, dxs, T(0));
+    chain16(acc, zb, cr.ab);
+    T acc8 = (gaps ? cr.g8 : T(0)) + cr.c88 * dx8;
+    chain16(acc8, zb, cr.ab8);
+    dxs = acc;
+    dx8 = acc8;
+    fin = fin && ((dxs - dxs) == T(0)) && ((dx8 - dx8) == T(0));
+  }
+  if (STEP && r.valid) {
+    r.w.DDX[(int64_t)N * NX17 + s] = dxs;
+    if (t == 0) r.w.DDX[(int64_t)N * NX17 + OM] = dx8;
+  }
+  if (!STEP && !OUT && r.valid) {
+    r.w.DX[(int64_t)N * NX17 + s] = dxs;
+    if (t == 0) r.w.DX[(int64_t)N * NX17 + OM] = dx8;
+  }
+  if (OUT && write && a.X) {
+    T* xo = a.X + (b * (int64_t)(N + 1) + N) * NX17;
+    xo[s] = r.w.XB[(int64_t)N * NX17 + s] + dxs;
+    if (t == 0) xo[OM] = r.w.XB[(int64_t)N * NX17 + OM] + dx8;
+  }
+  return fin;
+}
+
+// The interior point of mpcb_full.hip riccati17_kernel<T, true> (same iteration as
+// oracle.ocp.ipm_box_solve) in this layout: input rows owned by the input lanes, state rows by the
+// owner of the state, the rows of state 8 spread over the lanes by stage (k = 1 + t, 1 + t + 16 ..).
+template <class T, bool BOX>
+__global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
+  __shared__ Lds<T> lds_all[GR];
+  __shared__ T sQ[NX17 * NX17];
+  __shared__ T sR[NU17 * NU17];
+  const int lane = threadIdx.x;
+  const int q = lane / LN;
+  const int t = lane % LN;
+  const int64_t c_raw = (int64_t)blockIdx.x * GR + q;
+  const bool valid = c_raw < a.nb;
+  const int64_t c = valid ? c_raw : a.nb - 1;   // a ragged last wave shadows the last instance
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const Weights17<T>& W = *a.W;
+  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const bool in = t >= 8 && t < 14;
+  const int s = sown(t);
+  const int m = in ? t - 8 : 0;
+  for (int e = lane; e < NX17 * NX17; e += 64) sQ[e] = a.s * W.Q[e];
+  for (int e = lane; e < NU17 * NU17; e += 64) sR[e] = a.s * W.R[e];
+  __syncthreads();
+  const Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
+                 lds_all[q], sQ, sR, t, s, zcol(t), m, in, valid};
+  Lds<T>& L = r.L;
+  const T* x0 = a.x0 + b * a.x0_sb;
+  const T dx0s = iterate ? x0[s] - r.w.XB[s] : T(0);
+  const T dx08 = iterate ? x0[OM] - r.w.XB[OM] : T(0);
+  int32_t st = MPCB_STATUS_OK;
+  bool fin;
+  if constexpr (!BOX) {
+    if (!backward<T>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
+    __syncthreads();   // K and k are read back across lanes
+    fin = forward<T, true, false, true>(r, dx0s, dx08, valid);
+  } else {
+    const T lbm = W.lbu[m], ubm = W.ubu[m];
+    // start: du strictly inside the box, lambda = 1; dx by the dynamics
+    if (valid && in) {
+      for (int k = 0; k < N; ++k) {
+        const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+        const T lb = lbm - ubk, ub = ubm - ubk, wd = ub - lb;
+        T* ip = r.w.IP + (int64_t)k * 18;
+        ip[m] = fmin(fmax(T(0), lb + T(IPM17_THETA) * wd), ub - T(IPM17_THETA) * wd);
+        ip[6 + m] = T(1);
+        ip[12 + m] = T(1);
+      }
+    }
+    __syncthreads();
+    forward<T, false, false, false>(r, dx0s, dx08, false);   // DX of the starting point
+    __syncthreads();
+    const bool sbox = a.sbox != 0;
+    // state rows: s = max(distance to the bound, theta w), lambda = 1
+    auto srow_init = [&](int k, int i) {
+      const T xb = r.w.XB[(int64_t)k * NX17 + i], y = r.w.DX[(int64_t)k * NX17 + i];
+      const T lb = W.lbx[i] - xb, ub = W.ubx[i] - xb, tw = T(IPM17_THETA) * (ub - lb);
+      T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
+      ix[0] = fmax(y - lb, tw);
+      ix[NX17] = fmax(ub - y, tw);
+      ix[2 * NX17] = T(1);
+      ix[3 * NX17] = T(1);
+    };
+    if (valid && sbox) {
+      for (int k = 1; k < N; ++k) srow_init(k, s);
+      for (int k = 1 + t; k < N; k += LN) srow_init(k, OM);
+    }
+    __syncthreads();
+    const T rows = T(N * NU17 + (sbox ? (N - 1) * NX17 : 0));
+    bool done = false;
+    T prev_alpha = T(1);
+    int nshort = 0;
+    constexpr bool F64 = sizeof(T) == 8;
+    const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
+    const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
+    for (int it = 0; it < a.max_as_iter; ++it) {
+      // duality measure mu = mean(lambda s), primal residual of the state rows
+      T part = T(0), res = T(0);
+      if (in) {
+#pragma unroll 4
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+          const T* ip = r.w.IP + (int64_t)k * 18;
+          part += ip[6 + m] * (ip[m] - (lbm - ubk)) + ip[12 + m] * ((ubm - ubk) - ip[m]);
+        }
+      }
+      if (sbox) {
+        auto acc_row = [&](int k, int i) {
+          const SRow<T> sr(r, k, i);
+          part += sr.ll * sr.sl + sr.lu * sr.su;
+          res = fmax(res, fmax(fabs(sr.rl), fabs(sr.ru)));
+        };
+#pragma unroll 4
+        for (int k = 1; k < N; ++k) acc_row(k, s);
+        for (int k = 1 + t; k < N; k += LN) acc_row(k, OM);
+      }
+      const T mu = row_sum(part) / (T(2) * rows);
+      if (sbox) res = row_max(res);
+      done = done || (!(mu > ipm_tol) && !(res > ipm_res));
+      if (__all(done || !valid)) break;
+      // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
+      const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
+      if (!backward<T>(r, smu) && !done) {
+        // a Newton system that lost positive definiteness near the solution: keep the current
+        // iterate as converged; earlier it is a failure
+        if (!(mu > ipm_brk) && !(res > ipm_res)) done = true;
+        else st = MPCB_STATUS_QP_FAIL;
+      }
+      __syncthreads();
+      forward<T, true, true, false>(r, T(0), T(0), false);   // the Newton step -> DDX, DDU
+      __syncthreads();
+      // step length: fraction tau to the boundary, primal and dual, common to the instance
+      T amax = T(1) / T(IPM17_TAU);
+      bool dfin = true;   // a finite direction from strictly positive slacks
+      if (in) {
+#pragma unroll 4
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+          const T* ip = r.w.IP + (int64_t)k * 18;
+          const T d = r.w.DDU[(int64_t)k * NU17 + m];
+          const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
+          const T ll = ip[6 + m], lu = ip[12 + m];
+          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          dfin = dfin && sl > T(0) && su > T(0) && (d - d) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
+          if (d < T(0)) amax = fmin(amax, -sl / d);
+          if (d > T(0)) amax = fmin(amax, su / d);
+          if (dll < T(0)) amax = fmin(amax, -ll / dll);
+          if (dlu < T(0)) amax = fmin(amax, -lu / dlu);
+        }
+      }
+      if (sbox) {
+        auto step_row = [&](int k, int i) {
+          const SRow<T> sr(r, k, i);
+          const T dy = r.w.DDX[(int64_t)k * NX17 + i];
+          const T dsl = dy + sr.rl, dsu = sr.ru - dy;
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          dfin = dfin && (dsl - dsl) == T(0) && (dsu - dsu) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
+          if (dsl < T(0)) amax = fmin(amax, -sr.sl / dsl);
+          if (dsu < T(0)) amax = fmin(amax, -sr.su / dsu);
+          if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
+          if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
+        };
+#pragma unroll 4
+        for (int k = 1; k < N; ++k) step_row(k, s);
+        for (int k = 1 + t; k < N; k += LN) step_row(k, OM);
+      }
+      amax = row_min(amax);
+      const int dbad = row_or(dfin ? 0 : 1);
+      // (a finished instance skips the updates: its Newton step may be non-finite)
+      const T alpha = fmin(T(1), T(IPM17_TAU) * amax);
+      prev_alpha = alpha;
+      if (!done && dbad) {   // no usable direction: converged near the solution, else a failure
+        if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
+        done = true;
+      }
+      nshort = (alpha < T(IPM17_SHORT)) ? nshort + 1 : 0;
+      if (!done && (alpha < T(IPM17_STALL) || nshort >= IPM17_SHORT_RUN)) {
+        // collapsed step, or a run of short ones: converged near the solution (conditioning
+        // limit), else an infeasible QP
+        if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
+        done = true;
+      }
+      if (!done && valid && in) {
+#pragma unroll 4
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+          T* ip = r.w.IP + (int64_t)k * 18;
+          const T d = r.w.DDU[(int64_t)k * NU17 + m];
+          const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
+          const T ll = ip[6 + m], lu = ip[12 + m];
+          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          ip[m] += alpha * d;
+          ip[6 + m] = ll + alpha * dll;
+          ip[12 + m] = lu + alpha * dlu;
+        }
+      }
+      if (!done && valid && sbox) {   // state-row slacks and multipliers (before DX moves)
+        auto upd_row = [&](int k, int i) {
+          const SRow<T> sr(r, k, i);
+          const T dy = r.w.DDX[(int64_t)k * NX17 + i];
+          const T dsl = dy + sr.rl, dsu = sr.ru - dy;
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
+          ix[0] = sr.sl + alpha * dsl;
+          ix[NX17] = sr.su + alpha * dsu;
+          ix[2 * NX17] = sr.ll + alpha * dll;
+          ix[3 * NX17] = sr.lu + alpha * dlu;
+        };
+#pragma unroll 4
+        for (int k = 1; k < N; ++k) upd_row(k, s);
+        for (int k = 1 + t; k < N; k += LN) upd_row(k, OM);
+      }
+      __syncthreads();   // the rows of state 8 are read by every lane of the next backward
+      if (!done && valid) {
+        for (int k = 0; k <= N; ++k) r.w.DX[(int64_t)k * NX17 + s] += alpha * r.w.DDX[(int64_t)k * NX17 + s];
+        for (int k = t; k <= N; k += LN) r.w.DX[(int64_t)k * NX17 + OM] += alpha * r.w.DDX[(int64_t)k * NX17 + OM];
+      }
+      __syncthreads();
+    }
+    if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+    // outputs: X = xbar + dx, U = ubar + du of the final iterate
+    fin = true;
+    for (int k = 0; k <= N; ++k) {
+      const T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
+      if (valid && a.X) {
+        T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
+        xo[s] = r.w.XB[(int64_t)k * NX17 + s] + xs;
+        if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + x8;
+      }
+      fin = fin && ((xs - xs) == T(0)) && ((x8 - x8) == T(0));
+      if (in && k < N) {
+        const T uo = r.w.UB[(int64_t)k * NU17 + m] + r.w.IP[(int64_t)k * 18 + m];
+        fin = fin && ((uo - uo) == T(0));
+        if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + m] = uo;
+        if (valid && k == 0) a.u0[b * NU17 + m] = uo;
+      }
+    }
+  }
+  // instance status: any lane's non-finite value marks the instance
+  const int bad = row_or(fin ? 0 : 1);
+  if (valid && t == 0) a.status[b] = bad ? MPCB_STATUS_NAN : st;
+}
+
+}  // namespace q17
+
+template <class T> hipError_t launch_riccati17q(const FullArgs<T>& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.nb + q17::GR - 1) / q17::GR));
+  if (a.box)
+    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true>), grid, dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL((q17::riccati17q_kernel<T, false>), grid, dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+template hipError_t launch_riccati17q<double>(const FullArgs<double>&, hipStream_t);
+template hipError_t launch_riccati17q<float>(const FullArgs<float>&, hipStream_t);
+
+}  // namespace mpcb

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter passes (one rocprofv3 run per pass; gfx950 slot limits: SQ 8, TCC 4, GRBM 2) over a
-# short bench run.  Usage (on the GPU box): tools/profile_pmc.sh OUTDIR [bench args...]
+# short bench run.  Usage (on the GPU box): [PROG=tools/bench_full17.py] tools/profile_pmc.sh OUTDIR [bench args...]
 # Counters are collected in their own runs with --kernel-trace only (no sys/runtime trace).
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
@@ -18,6 +18,6 @@ PASSES=(
 i=0
 for P in "${PASSES[@]}"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --output-format csv -d "$OUT" -o pass$i -- python3 bench.py $ARGS > "$OUT/pass$i.log" 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $P --output-format csv -d "$OUT" -o pass$i -- python3 ${PROG:-bench.py} $ARGS > "$OUT/pass$i.log" 2>&1
 done
 echo done
