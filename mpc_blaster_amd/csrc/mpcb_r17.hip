@@ -36,6 +36,17 @@ namespace mpcb {
 namespace q17 {
 
 constexpr int LN = 16, GR = 64 / LN;   // lanes per instance, instances per wavefront
+#ifdef MPCB_Q17_STAMPS
+// Diagnostic build only: per-region s_memtime deltas of workgroup 0, printed at the end.
+#define QSTAMP_INIT() unsigned long long qs_prev = __builtin_amdgcn_s_memtime(), qs_acc[12] = {};
+#define QSTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); qs_acc[i] += t_ - qs_prev; qs_prev = t_; }
+#define QSTAMP_DONE(tag) if (blockIdx.x == 0 && threadIdx.x == 0) printf("QSTAMP %s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", tag, \
+    qs_acc[0], qs_acc[1], qs_acc[2], qs_acc[3], qs_acc[4], qs_acc[5], qs_acc[6], qs_acc[7], qs_acc[8], qs_acc[9], qs_acc[10], qs_acc[11]);
+#else
+#define QSTAMP_INIT()
+#define QSTAMP(i)
+#define QSTAMP_DONE(tag)
+#endif
 constexpr int OM = 8;                  // the state whose P column is held distributed
 
 // lane t -> z column of [A|B] it holds, state column of P it owns; state i -> owning lane
@@ -97,18 +108,21 @@ template <class T> __device__ __forceinline__ void diag16_sown(T (&y)[NX17], T a
   if constexpr (sizeof(T) == 8) Q17_D16("v_fmac_f64_dpp", Q17_YS16); else Q17_D16("v_fmac_f32_dpp", Q17_YS16);
 }
 
-// acc += bcast_t(a) * w[t] for the 16 lanes t of the row (one dependent chain)
+// acc += sum_t bcast_t(a) * w[t] over the 16 lanes t of the row: four interleaved partial sums
+// (a single dependent chain of 16 DPP FMAs costs the forward pass its latency)
 #define Q17_C16(OP)                                                                                      \
-  asm("s_nop 4\n\t" Q17_BC(OP, 0, 1, 2, "0") Q17_BC(OP, 0, 1, 3, "1") Q17_BC(OP, 0, 1, 4, "2")           \
-      Q17_BC(OP, 0, 1, 5, "3") Q17_BC(OP, 0, 1, 6, "4") Q17_BC(OP, 0, 1, 7, "5") Q17_BC(OP, 0, 1, 8, "6") \
-      Q17_BC(OP, 0, 1, 9, "7") Q17_BC(OP, 0, 1, 10, "8") Q17_BC(OP, 0, 1, 11, "9")                       \
-      Q17_BC(OP, 0, 1, 12, "10") Q17_BC(OP, 0, 1, 13, "11") Q17_BC(OP, 0, 1, 14, "12")                   \
-      Q17_BC(OP, 0, 1, 15, "13") Q17_BC(OP, 0, 1, 16, "14") Q17_BC(OP, 0, 1, 17, "15")                   \
-      : "+v"(acc)                                                                                        \
+  asm("s_nop 4\n\t" Q17_BC(OP, 0, 4, 5, "0") Q17_BC(OP, 1, 4, 6, "1") Q17_BC(OP, 2, 4, 7, "2")           \
+      Q17_BC(OP, 3, 4, 8, "3") Q17_BC(OP, 0, 4, 9, "4") Q17_BC(OP, 1, 4, 10, "5") Q17_BC(OP, 2, 4, 11, "6") \
+      Q17_BC(OP, 3, 4, 12, "7") Q17_BC(OP, 0, 4, 13, "8") Q17_BC(OP, 1, 4, 14, "9")                       \
+      Q17_BC(OP, 2, 4, 15, "10") Q17_BC(OP, 3, 4, 16, "11") Q17_BC(OP, 0, 4, 17, "12")                   \
+      Q17_BC(OP, 1, 4, 18, "13") Q17_BC(OP, 2, 4, 19, "14") Q17_BC(OP, 3, 4, 20, "15")                   \
+      : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)                                                            \
       : "v"(a), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]),  \
         "v"(w[8]), "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]))
 template <class T> __device__ __forceinline__ void chain16(T& acc, T a, const T (&w)[LN]) {
+  T p0 = acc, p1 = T(0), p2 = T(0), p3 = T(0);
   if constexpr (sizeof(T) == 8) Q17_C16("v_fmac_f64_dpp"); else Q17_C16("v_fmac_f32_dpp");
+  acc = (p0 + p1) + (p2 + p3);
 }
 
 // lane L's v in every lane of the row (0 + bcast_L(v) * 1: exact)
@@ -270,6 +284,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
   bool qp_ok = true;
   Pre<T> nx;
   prefetch(r, N - 1, nx);
+  QSTAMP_INIT();
   for (int k = N - 1; k >= 0; --k) {
     const Pre<T> cu = nx;
     prefetch(r, k > 0 ? k - 1 : 0, nx);   // (unconditional: no branch join on the loads)
@@ -285,6 +300,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
       for (int i = 0; i < NX17; ++i) pt += Pc[i] * gk[i];
       pt8 += P88 * gk[OM] + row_sum(prow);
     }
+    QSTAMP(0);
     // ---- Y = P [A|B]_z and h_AB = [A|B]_z^T pt
     T y[NX17], hab = T(0);
 #pragma unroll
@@ -296,6 +312,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
     diag16_sown(y, Pc[OM], cu.ab[OM]);
     y[OM] += P88 * cu.ab[OM];
     hab += pt8 * cu.ab[OM];
+    QSTAMP(1);
     // ---- G_z = [A|B]^T Y_z: rows z(t') by row broadcasts of [A|B] columns, identity rows = Y rows,
     // row 8 by the shear column
     T g[LN];
@@ -306,6 +323,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
     T g8 = T(0);
 #pragma unroll
     for (int q = 0; q < 5; ++q) g8 += cu.a8[q] * y[c8row(q)];
+    QSTAMP(2);
     // identity rows of this lane's Y for the identity-state lanes (their G column, by symmetry)
 #pragma unroll
     for (int ci = 0; ci < 6; ++ci) L.YC[ci][t] = y[ids(ci)];
@@ -329,6 +347,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
       L.HU[m][7] = g8;
     }
     wave_lds_sync();
+    QSTAMP(3);
     // ---- this lane's state column Gs = G[:, s] (23 rows by z index) and gradient h_s
     T Gs[NZ17];
     {
@@ -380,6 +399,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
       G88 += D;
       h8 += d;
     }
+    QSTAMP(4);
     // ---- Huu (lower triangle from the column owners), Cholesky, k, K columns
     T H[NU17 * NU17], hu[NU17], hx8[NU17];
 #pragma unroll
@@ -405,6 +425,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
 #pragma unroll
     for (int i = 0; i < NU17; ++i) nb[i] = -hx8[i];
     chol_n_solve<T, NU17>(Lc, nb, K8);
+    QSTAMP(5);
     if (r.valid) {   // KR: K row-major [6][17], then k[6]
       T* kr = r.w.KR + (int64_t)k * KR_N;
 #pragma unroll
@@ -415,6 +436,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
       }
       if (in) kr[NU17 * NX17 + r.m] = sel<NU17>(kff, r.m);
     }
+    QSTAMP(6);
     // ---- P_new[:, s] = G_xx[:, s] + Hxu K[:, s]; p_new; the 8 entries
     T Pn[NX17];
 #pragma unroll
@@ -456,7 +478,9 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
     pj = pn;
     p8 = pn8;
     wave_lds_sync();
+    QSTAMP(7);
   }
+  QSTAMP_DONE("bwd");
   return qp_ok;
 }
 
@@ -475,7 +499,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   const uint64_t m_in = lane_mask(in), m_id = m_in;   // identity-state lanes = input lanes
   bool fin = true;
   // stage rows one stage ahead: K row m and k_m (input lanes), row s and row 8 of [A|B]
-  struct Row { T kr[LN], k8, kf, du, ab[LN], ab8[LN], c8s, c88, gs, g8; };
+  struct Row { T kr[LN], k8, kf, du, ab[LN], ab8[LN], c8s, c88, gs, g8, xbs, xb8, ubm; };
   auto load = [&](int k, Row& o) {
     const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
     if constexpr (GAIN) {
@@ -495,13 +519,18 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     o.c8s = ABk[OM * NX17 + s];
     o.c88 = ABk[OM * NX17 + OM];
     o.gs = r.w.GP[(int64_t)k * NX17 + s];   // (raw: selected at use)
+    o.xbs = r.w.XB[(int64_t)k * NX17 + s];
+    o.xb8 = r.w.XB[(int64_t)k * NX17 + OM];
+    o.ubm = r.w.UB[(int64_t)k * NU17 + r.m];
     o.g8 = r.w.GP[(int64_t)k * NX17 + OM];
   };
   Row nr;
   load(0, nr);
+  QSTAMP_INIT();
   for (int k = 0; k < N; ++k) {
     const Row cr = nr;
     if (k + 1 < N) load(k + 1, nr);
+    QSTAMP(0);
     T du;
     if constexpr (GAIN) {
       du = cr.kf + cr.k8 * dx8;
@@ -521,11 +550,11 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     }
     if (OUT && write && a.X) {
       T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
-      xo[s] = r.w.XB[(int64_t)k * NX17 + s] + dxs;
-      if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + dx8;
+      xo[s] = cr.xbs + dxs;
+      if (t == 0) xo[OM] = cr.xb8 + dx8;
     }
     if (in) {
-      const T uo = r.w.UB[(int64_t)k * NU17 + r.m] + du;
+      const T uo = cr.ubm + du;
       fin = fin && ((uo - uo) == T(0));
       if (OUT && write && a.U) a.U[(b * (int64_t)N + k) * NU17 + r.m] = uo;
       if (OUT && write && k == 0) a.u0[b * NU17 + r.m] = uo;
@@ -539,7 +568,9 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     dxs = acc;
     dx8 = acc8;
     fin = fin && ((dxs - dxs) == T(0)) && ((dx8 - dx8) == T(0));
+    QSTAMP(1);
   }
+  QSTAMP_DONE("fwd");
   if (STEP && r.valid) {
     r.w.DDX[(int64_t)N * NX17 + s] = dxs;
     if (t == 0) r.w.DDX[(int64_t)N * NX17 + OM] = dx8;
