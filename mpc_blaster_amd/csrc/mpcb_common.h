@@ -8,11 +8,16 @@
 
 namespace mpcb {
 
+// Row strides of the per-lane LDS rows written by all 16 lanes of a group at once: NX + 1 and
+// NU + 1 put the 16 rows on distinct bank pairs (ds_write_b64 / ds_write_b32 bank = dword mod 32;
+// the unpadded 12- and 4-element rows were 4-way conflicts: SQ_LDS_BANK_CONFLICT 54 % of P2's
+// LDS cycles at c2, profiles/pmc_c2.json).
+constexpr int XS = NX + 1, HS = NU + 1;
 template <class T>
 struct GroupLds {
   T P[NX * NX];   // value-function Hessian, P[l*NX + i] = column l (symmetric)
-  T X[NZ * NX];   // X[j*NX + i] = ([A|B])_{i j}
-  T Hu[NZ * NU];  // Hu[j*NU + m] = G_{NX+m, j}   (H_ux columns, then H_uu)
+  T X[NZ * XS];   // X[j*XS + i] = ([A|B])_{i j} (split path; the other kernels use stride NX)
+  T Hu[NZ * HS];  // Hu[j*HS + m] = G_{NX+m, j}   (H_ux columns, then H_uu; split path stride)
   T v[NZ];        // vector exchange (e = ybar - yref, then pt = p + P b)
   T hv[NZ];       // gradient h = [h_x; h_u]
 };

@@ -470,7 +470,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // LDS-operand fp64 products
 #pragma unroll
-      for (int i = 0; i < NX; ++i) L.X[j * NX + i] = col[i];
+      for (int i = 0; i < NX; ++i) L.X[j * XS + i] = col[i];
     }
     wave_lds_sync();
     STAMP(2);
@@ -517,7 +517,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NZ; ++i) {
         T acc = T(0);
 #pragma unroll
-        for (int l = 0; l < NX; ++l) acc += L.X[i * NX + l] * y[l];
+        for (int l = 0; l < NX; ++l) acc += L.X[i * XS + l] * y[l];
         G[i] = acc;
       }
     }
@@ -539,7 +539,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       stv<T, 20>(rec2(a.GH, k, GH2_REC, nb, c) + ju * 20, row);
     }
 #pragma unroll
-    for (int m = 0; m < NU; ++m) L.Hu[j * NU + m] = G[NX + m];
+    for (int m = 0; m < NU; ++m) L.Hu[j * HS + m] = G[NX + m];
     wave_lds_sync();
     L.hv[j] = hj;
     wave_lds_sync();
@@ -548,7 +548,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
     for (int m = 0; m < NU; ++m) {
 #pragma unroll
-      for (int n = 0; n < NU; ++n) Huu[m * NU + n] = L.Hu[(NX + n) * NU + m];
+      for (int n = 0; n < NU; ++n) Huu[m * NU + n] = L.Hu[(NX + n) * HS + m];
       hu[m] = -L.hv[NX + m];
     }
     T Lc[10];
@@ -578,7 +578,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NX; ++i) {
         T acc = G[i];
 #pragma unroll
-        for (int m = 0; m < NU; ++m) acc += L.Hu[i * NU + m] * Kj[m];
+        for (int m = 0; m < NU; ++m) acc += L.Hu[i * HS + m] * Kj[m];
         Pn[i] = acc;
       }
     }
@@ -609,7 +609,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     // own them: uniform code instead of per-entry predicated stores.  (L.X is free: this
     // stage's products are done.)
 #pragma unroll
-    for (int i = 0; i < NX; ++i) L.X[j * NX + i] = Pn[i];
+    for (int i = 0; i < NX; ++i) L.X[j * XS + i] = Pn[i];
     pj = pn;
     if (k > 0) commit(buf ^ 1);
     wave_lds_sync();
@@ -619,13 +619,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       const uint64_t st_lane = lane_mask(j < NX);
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
-        const T o = L.X[i * NX + jx];
+        const T o = L.X[i * XS + jx];
         Pc[i] = csel(st_lane, csel(lane_mask(i <= j), Pn[i], o), T(0));
       }
     }
 #else
 #pragma unroll
-    for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * NX + j]) : T(0);
+    for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * XS + j]) : T(0);
 #endif
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // the LDS fp64 products read P from LDS
       if (j < NX) {
