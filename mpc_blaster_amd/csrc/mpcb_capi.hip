@@ -211,7 +211,8 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     h->split = 1;
     if (const char* e = getenv("MPCB_R17")) h->q17 = atoi(e) != 0;
     h->chunk = chunk;
-    h->chunk_elems = full17_elems(cfg->N) * chunk;
+    // (+3 instances: a ragged last wavefront of the 16-lane kernel works in private padding slots)
+    h->chunk_elems = full17_elems(cfg->N) * ((chunk + 3) / 4 * 4);
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
   int64_t split_min = 1;

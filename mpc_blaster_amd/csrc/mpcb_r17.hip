@@ -32,6 +32,15 @@
 #include "mpcb_common.h"
 #include "mpcb_full.h"
 
+// forward-pass ring depths (stages of row loads in flight): the unconstrained pass, the interior
+// point's Newton-step pass
+#ifndef MPCB_Q17_FD
+#define MPCB_Q17_FD 3
+#endif
+#ifndef MPCB_Q17_FD_STEP
+#define MPCB_Q17_FD_STEP 3
+#endif
+
 namespace mpcb {
 namespace q17 {
 
@@ -125,6 +134,23 @@ template <class T> __device__ __forceinline__ void chain16(T& acc, T a, const T 
   acc = (p0 + p1) + (p2 + p3);
 }
 
+// sum over the 16 lanes of the row of v (every lane gets it): four interleaved DPP partial sums
+#define Q17_S16(OP)                                                                                      \
+  asm("s_nop 4\n\t" Q17_BC(OP, 0, 4, 5, "0") Q17_BC(OP, 1, 4, 5, "1") Q17_BC(OP, 2, 4, 5, "2")           \
+      Q17_BC(OP, 3, 4, 5, "3") Q17_BC(OP, 0, 4, 5, "4") Q17_BC(OP, 1, 4, 5, "5") Q17_BC(OP, 2, 4, 5, "6")  \
+      Q17_BC(OP, 3, 4, 5, "7") Q17_BC(OP, 0, 4, 5, "8") Q17_BC(OP, 1, 4, 5, "9")                        \
+      Q17_BC(OP, 2, 4, 5, "10") Q17_BC(OP, 3, 4, 5, "11") Q17_BC(OP, 0, 4, 5, "12")                     \
+      Q17_BC(OP, 1, 4, 5, "13") Q17_BC(OP, 2, 4, 5, "14") Q17_BC(OP, 3, 4, 5, "15")                     \
+      : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)                                                          \
+      : "v"(v), "v"(one))
+template <class T> __device__ __forceinline__ T sum16(T v, T init = T(0)) {
+  T p0 = init, p1 = T(0), p2 = T(0), p3 = T(0);
+  const T one = T(1);
+  if constexpr (sizeof(T) == 8) Q17_S16("v_fmac_f64_dpp"); else Q17_S16("v_fmac_f32_dpp");
+  return (p0 + p1) + (p2 + p3);
+}
+#undef Q17_S16
+
 // lane L's v in every lane of the row (0 + bcast_L(v) * 1: exact)
 template <int L, class T> __device__ __forceinline__ T bcast(T v) {
   T r = T(0);
@@ -201,16 +227,12 @@ struct SRow {
 };
 
 // Stage data loaded one stage ahead, as raw loads: every value is consumed a stage later (any
-// arithmetic or select on a load here would wait for it on the spot).  The interior point's
-// iterate, multipliers and state-row slacks are loaded unconditionally (the workspace always holds
-// them; unused values are discarded by selects, never multiplied).
+// arithmetic or select on a load here would wait for it on the spot).
 template <class T>
 struct Pre {
   T ab[NX17];      // column z of [A_k | B_k]
   T a8[5];         // the nonzeros of the implicit column 8 (rows c8row(0..4))
   T xs, x8, xrs, xr8, ub, urm;          // xbar_k[s], xbar_k[8], xref_k[s], xref_k[8], ubar_k[m], uref_k[m]
-  T dxs, dx8, du, ll, lu;               // interior point: dx_k[s], dx_k[8], (du, lambda_l, lambda_u)_k[m]
-  T ixs[4], ix8[4];                     // state rows (s_l, s_u, lambda_l, lambda_u) of s and 8
 };
 
 template <class T>
@@ -227,6 +249,19 @@ __device__ __forceinline__ void prefetch(const Ctx<T>& r, int k, Pre<T>& p) {
   p.xr8 = r.xr[kx + OM];
   p.ub = r.w.UB[(int64_t)k * NU17 + r.m];
   p.urm = r.ur[(int64_t)k * NU17 + r.m];
+}
+
+// The interior point's iterate, multipliers and state-row slacks of the current stage: loaded at
+// the top of the stage and consumed after the two product passes (they are not carried a stage
+// ahead: that register set pushed the fp64 interior-point kernel into scratch)
+template <class T>
+struct Cur {
+  T dxs, dx8, du, ll, lu;               // dx_k[s], dx_k[8], (du, lambda_l, lambda_u)_k[m]
+  T ixs[4], ix8[4];                     // state rows (s_l, s_u, lambda_l, lambda_u) of s and 8
+};
+template <class T>
+__device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
+  const int64_t kx = (int64_t)k * NX17;
   p.dxs = r.w.DX[kx + r.s];
   p.dx8 = r.w.DX[kx + OM];
   const T* ip = r.w.IP + (int64_t)k * 18;
@@ -288,10 +323,9 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
   for (int k = N - 1; k >= 0; --k) {
     const Pre<T> cu = nx;
     prefetch(r, k > 0 ? k - 1 : 0, nx);   // (unconditional: no branch join on the loads)
-    // cost residual into LDS (general Q, R); pt = p + P gap (iterate mode)
-    L.V[s] = (ipm ? cu.xs + cu.dxs : cu.xs) - cu.xrs;
-    L.V[OM] = (ipm ? cu.x8 + cu.dx8 : cu.x8) - cu.xr8;
-    if (in) L.V[NX17 + r.m] = (ipm ? cu.ub + cu.du : cu.ub) - cu.urm;
+    Cur<T> ic;
+    if (ipm) load_cur(r, k, ic);
+    // pt = p + P gap (iterate mode)
     T pt = pj, pt8 = p8;
     if (gaps) {
       const T* gk = r.w.GP + (int64_t)k * NX17;
@@ -324,6 +358,10 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) g8 += cu.a8[q] * y[c8row(q)];
     QSTAMP(2);
+    // cost residual (ybar [+ iterate] - yref) into LDS (general Q, R)
+    L.V[s] = (ipm ? cu.xs + ic.dxs : cu.xs) - cu.xrs;
+    L.V[OM] = (ipm ? cu.x8 + ic.dx8 : cu.x8) - cu.xr8;
+    if (in) L.V[NX17 + r.m] = (ipm ? cu.ub + ic.du : cu.ub) - cu.urm;
     // identity rows of this lane's Y for the identity-state lanes (their G column, by symmetry)
 #pragma unroll
     for (int ci = 0; ci < 6; ++ci) L.YC[ci][t] = y[ids(ci)];
@@ -339,8 +377,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
         L.HU[m][n] = g[8 + n] + wr;
       }
       if (ipm) {
-        const T sl = cu.du - (lbm - cu.ub), su = (ubm - cu.ub) - cu.du;
-        L.HU[m][m] += cu.ll / sl + cu.lu / su;
+        const T sl = ic.du - (lbm - cu.ub), su = (ubm - cu.ub) - ic.du;
+        L.HU[m][m] += ic.ll / sl + ic.lu / su;
         hu -= smu * (T(1) / sl - T(1) / su);
       }
       L.HU[m][6] = hu;
@@ -391,11 +429,11 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
     }
     if (sbox && k > 0) {   // state-box rows of this stage: barrier terms on the state diagonals
       T D, d;
-      SRow<T>(cu.dxs, cu.xs, lbs, ubs, cu.ixs[0], cu.ixs[1], cu.ixs[2], cu.ixs[3]).barrier(smu, D, d);
+      SRow<T>(ic.dxs, cu.xs, lbs, ubs, ic.ixs[0], ic.ixs[1], ic.ixs[2], ic.ixs[3]).barrier(smu, D, d);
 #pragma unroll
       for (int i = 0; i < NX17; ++i) Gs[i] += (i == s) ? D : T(0);
       hs += d;
-      SRow<T>(cu.dx8, cu.x8, lb8, ub8, cu.ix8[0], cu.ix8[1], cu.ix8[2], cu.ix8[3]).barrier(smu, D, d);
+      SRow<T>(ic.dx8, cu.x8, lb8, ub8, ic.ix8[0], ic.ix8[1], ic.ix8[2], ic.ix8[3]).barrier(smu, D, d);
       G88 += D;
       h8 += d;
     }
@@ -426,15 +464,16 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
     for (int i = 0; i < NU17; ++i) nb[i] = -hx8[i];
     chol_n_solve<T, NU17>(Lc, nb, K8);
     QSTAMP(5);
-    if (r.valid) {   // KR: K row-major [6][17], then k[6]
+    {   // KR: K row-major [6][17], then k[6].  Unconditional stores (a padding group owns its slot):
+        // the K column of state 8 and k are the same in every lane (each lane solved the same
+        // 6x6 systems), so every lane writes them to a fixed or its own input's slot
       T* kr = r.w.KR + (int64_t)k * KR_N;
 #pragma unroll
-      for (int i = 0; i < NU17; ++i) kr[i * NX17 + s] = Ks[i];
-      if (t == 0) {
-#pragma unroll
-        for (int i = 0; i < NU17; ++i) kr[i * NX17 + OM] = K8[i];
+      for (int i = 0; i < NU17; ++i) {
+        kr[i * NX17 + s] = Ks[i];
+        kr[i * NX17 + OM] = K8[i];
       }
-      if (in) kr[NU17 * NX17 + r.m] = sel<NU17>(kff, r.m);
+      kr[NU17 * NX17 + r.m] = sel<NU17>(kff, r.m);
     }
     QSTAMP(6);
     // ---- P_new[:, s] = G_xx[:, s] + Hxu K[:, s]; p_new; the 8 entries
@@ -498,8 +537,11 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   const int64_t b = a.b0 + (r.w.XB - a.ws) / full17_elems(N);
   const uint64_t m_in = lane_mask(in), m_id = m_in;   // identity-state lanes = input lanes
   bool fin = true;
-  // stage rows one stage ahead: K row m and k_m (input lanes), row s and row 8 of [A|B]
-  struct Row { T kr[LN], k8, kf, du, ab[LN], ab8[LN], c8s, c88, gs, g8, xbs, xb8, ubm; };
+  // Stage rows FD stages ahead in a ring of register slots, the stage loop unrolled by FD so every
+  // slot is a fixed register set (a copy of a slot would wait for its loads on the spot): K row m
+  // and k_m (input lanes), row s of [A|B] at the lanes' z columns, the own entry of row 8
+  constexpr int FD = STEP ? MPCB_Q17_FD_STEP : MPCB_Q17_FD;
+  struct Row { T kr[LN], k8, kf, du, ab[LN], ab8o, c8s, c88, gs, g8, xbs, xb8, ubm; };
   auto load = [&](int k, Row& o) {
     const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
     if constexpr (GAIN) {
@@ -512,24 +554,23 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
       o.du = r.w.IP[(int64_t)k * 18 + r.m];
     }
 #pragma unroll
-    for (int tp = 0; tp < LN; ++tp) {
-      o.ab[tp] = ABk[zcol(tp) * NX17 + s];
-      o.ab8[tp] = ABk[zcol(tp) * NX17 + OM];
-    }
+    for (int tp = 0; tp < LN; ++tp) o.ab[tp] = ABk[zcol(tp) * NX17 + s];
+    o.ab8o = ABk[r.z * NX17 + OM];
     o.c8s = ABk[OM * NX17 + s];
     o.c88 = ABk[OM * NX17 + OM];
     o.gs = r.w.GP[(int64_t)k * NX17 + s];   // (raw: selected at use)
+    o.g8 = r.w.GP[(int64_t)k * NX17 + OM];
     o.xbs = r.w.XB[(int64_t)k * NX17 + s];
     o.xb8 = r.w.XB[(int64_t)k * NX17 + OM];
     o.ubm = r.w.UB[(int64_t)k * NU17 + r.m];
-    o.g8 = r.w.GP[(int64_t)k * NX17 + OM];
   };
-  Row nr;
-  load(0, nr);
+  Row ring[FD];
+  T u0v = T(0);   // u_0 (OUT: written once after the pass)
+  static_for<FD>([&](auto sl) {
+    if (decltype(sl)::value < N) load(decltype(sl)::value, ring[decltype(sl)::value]);
+  });
   QSTAMP_INIT();
-  for (int k = 0; k < N; ++k) {
-    const Row cr = nr;
-    if (k + 1 < N) load(k + 1, nr);
+  auto stage = [&](int k, Row& cr) {
     QSTAMP(0);
     T du;
     if constexpr (GAIN) {
@@ -539,50 +580,59 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
       du = cr.du;
     }
     if (!in) du = T(0);
-    if (STEP && r.valid) {
-      r.w.DDX[(int64_t)k * NX17 + s] = dxs;
-      if (t == 0) r.w.DDX[(int64_t)k * NX17 + OM] = dx8;
-      if (in) r.w.DDU[(int64_t)k * NU17 + r.m] = du;
+    // stores without lane-divergent branches (a branch around a store makes the vmcnt count of
+    // the ring's loads dynamic and every wait a vmcnt(0)): each lane stores its own state, and the
+    // input lanes' du or (every other lane, the same value) the state-8 entry
+    if constexpr (STEP || !OUT) {
+      T* base = STEP ? r.w.DDX : r.w.DX;
+      base[(int64_t)k * NX17 + s] = dxs;
+      T* p2 = (STEP && in) ? r.w.DDU + (int64_t)k * NU17 + r.m : base + (int64_t)k * NX17 + OM;
+      *p2 = (STEP && in) ? du : dx8;
     }
-    if (!STEP && !OUT && r.valid) {
-      r.w.DX[(int64_t)k * NX17 + s] = dxs;
-      if (t == 0) r.w.DX[(int64_t)k * NX17 + OM] = dx8;
-    }
-    if (OUT && write && a.X) {
-      T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
-      xo[s] = cr.xbs + dxs;
-      if (t == 0) xo[OM] = cr.xb8 + dx8;
+    if constexpr (OUT) {
+      // caller arrays for valid groups that asked for them, else this lane's own DDX slot
+      const bool wx = write && a.X, wu = write && a.U;
+      T* p1 = wx ? a.X + (b * (int64_t)(N + 1) + k) * NX17 + s : r.w.DDX + (int64_t)k * NX17 + s;
+      *p1 = cr.xbs + dxs;
+      T* p2 = in ? (wu ? a.U + (b * (int64_t)N + k) * NU17 + r.m : r.w.DDU + (int64_t)k * NU17 + r.m)
+                 : (wx ? a.X + (b * (int64_t)(N + 1) + k) * NX17 + OM : r.w.DDX + (int64_t)k * NX17 + OM);
+      *p2 = in ? cr.ubm + du : cr.xb8 + dx8;
+      if (k == 0) u0v = cr.ubm + du;
     }
     if (in) {
       const T uo = cr.ubm + du;
       fin = fin && ((uo - uo) == T(0));
-      if (OUT && write && a.U) a.U[(b * (int64_t)N + k) * NU17 + r.m] = uo;
-      if (OUT && write && k == 0) a.u0[b * NU17 + r.m] = uo;
     }
-    // dx' = [A|B] (dx, du) + gap: lanes broadcast their z value (du on input lanes)
+    // dx' = [A|B] (dx, du) + gap: lanes broadcast their z value (du on input lanes); row 8 as a
+    // row sum of the lanes' own terms
     const T zb = csel(m_in, du, dxs);
     T acc = (gaps ? cr.gs : T(0)) + cr.c8s * dx8 + csel(m_id, dxs, T(0));
     chain16(acc, zb, cr.ab);
-    T acc8 = (gaps ? cr.g8 : T(0)) + cr.c88 * dx8;
-    chain16(acc8, zb, cr.ab8);
+    const T acc8 = sum16(cr.ab8o * zb, (gaps ? cr.g8 : T(0)) + cr.c88 * dx8);
     dxs = acc;
     dx8 = acc8;
     fin = fin && ((dxs - dxs) == T(0)) && ((dx8 - dx8) == T(0));
+    if (k + FD < N) load(k + FD, cr);   // refill this slot FD stages ahead
     QSTAMP(1);
+  };
+  for (int k0 = 0; k0 < N; k0 += FD) {
+    static_for<FD>([&](auto sl) {
+      if (k0 + decltype(sl)::value < N) stage(k0 + decltype(sl)::value, ring[decltype(sl)::value]);
+    });
   }
   QSTAMP_DONE("fwd");
-  if (STEP && r.valid) {
-    r.w.DDX[(int64_t)N * NX17 + s] = dxs;
-    if (t == 0) r.w.DDX[(int64_t)N * NX17 + OM] = dx8;
+  if constexpr (STEP || !OUT) {
+    T* base = STEP ? r.w.DDX : r.w.DX;
+    base[(int64_t)N * NX17 + s] = dxs;
+    base[(int64_t)N * NX17 + OM] = dx8;
   }
-  if (!STEP && !OUT && r.valid) {
-    r.w.DX[(int64_t)N * NX17 + s] = dxs;
-    if (t == 0) r.w.DX[(int64_t)N * NX17 + OM] = dx8;
-  }
-  if (OUT && write && a.X) {
-    T* xo = a.X + (b * (int64_t)(N + 1) + N) * NX17;
-    xo[s] = r.w.XB[(int64_t)N * NX17 + s] + dxs;
-    if (t == 0) xo[OM] = r.w.XB[(int64_t)N * NX17 + OM] + dx8;
+  if constexpr (OUT) {
+    if (write && a.X) {
+      T* xo = a.X + (b * (int64_t)(N + 1) + N) * NX17;
+      xo[s] = r.w.XB[(int64_t)N * NX17 + s] + dxs;
+      if (t == 0) xo[OM] = r.w.XB[(int64_t)N * NX17 + OM] + dx8;
+    }
+    if (write && in) a.u0[b * NU17 + r.m] = u0v;
   }
   return fin;
 }
@@ -600,8 +650,11 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   const int t = lane % LN;
   const int64_t c_raw = (int64_t)blockIdx.x * GR + q;
   const bool valid = c_raw < a.nb;
-  const int64_t c = valid ? c_raw : a.nb - 1;   // a ragged last wave shadows the last instance
-  const int64_t b = a.b0 + c;
+  // a ragged last wave's extra groups run on private padding slots of the workspace (mpcb_create
+  // sizes it to whole wavefronts), so every workspace store is unconditional; their inputs and
+  // outputs are the last instance's
+  const int64_t c = c_raw;
+  const int64_t b = a.b0 + (valid ? c : a.nb - 1);
   const int N = a.N;
   const Weights17<T>& W = *a.W;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
@@ -662,7 +715,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     constexpr bool F64 = sizeof(T) == 8;
     const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
     const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
+    QSTAMP_INIT();
     for (int it = 0; it < a.max_as_iter; ++it) {
+      QSTAMP(6);
       // duality measure mu = mean(lambda s), primal residual of the state rows
       T part = T(0), res = T(0);
       if (in) {
@@ -687,6 +742,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       if (sbox) res = row_max(res);
       done = done || (!(mu > ipm_tol) && !(res > ipm_res));
       if (__all(done || !valid)) break;
+      QSTAMP(0);
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
       const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
       if (!backward<T>(r, smu) && !done) {
@@ -696,8 +752,10 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         else st = MPCB_STATUS_QP_FAIL;
       }
       __syncthreads();
+      QSTAMP(1);
       forward<T, true, true, false>(r, T(0), T(0), false);   // the Newton step -> DDX, DDU
       __syncthreads();
+      QSTAMP(2);
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       T amax = T(1) / T(IPM17_TAU);
       bool dfin = true;   // a finite direction from strictly positive slacks
@@ -735,6 +793,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         for (int k = 1 + t; k < N; k += LN) step_row(k, OM);
       }
       amax = row_min(amax);
+      QSTAMP(3);
       const int dbad = row_or(dfin ? 0 : 1);
       // (a finished instance skips the updates: its Newton step may be non-finite)
       const T alpha = fmin(T(1), T(IPM17_TAU) * amax);
@@ -782,12 +841,15 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         for (int k = 1 + t; k < N; k += LN) upd_row(k, OM);
       }
       __syncthreads();   // the rows of state 8 are read by every lane of the next backward
+      QSTAMP(4);
       if (!done && valid) {
         for (int k = 0; k <= N; ++k) r.w.DX[(int64_t)k * NX17 + s] += alpha * r.w.DDX[(int64_t)k * NX17 + s];
         for (int k = t; k <= N; k += LN) r.w.DX[(int64_t)k * NX17 + OM] += alpha * r.w.DDX[(int64_t)k * NX17 + OM];
       }
       __syncthreads();
     }
+    QSTAMP(5);
+    QSTAMP_DONE("ipm");
     if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
     // outputs: X = xbar + dx, U = ubar + du of the final iterate
     fin = true;
