@@ -88,9 +88,19 @@ def main():
     peak = 78.6 if args.dtype == 'f64' else 157.3
     roof = None
     if args.bounds == 'none':
+        # the 16-lane DPP kernel (mpcb_r17.hip) unless MPCB_R17=0; dense count over the kernel's
+        # HIP-event time; executed_frac from the committed PMC summary (profiles/pmc_full17.json,
+        # 64 x SQ_INSTS_VALU_FLOPS_FP64 per launch: the kernel skips the 9 structural columns)
+        q17 = os.environ.get('MPCB_R17', '1') != '0'
+        kname = ('q17::riccati17q_kernel' if q17 else 'riccati17_kernel') + f'<{"double" if args.dtype == "f64" else "float"}, false>'
         ach = fl * N * B / (ph['riccati'] * 1e-3) / 1e12
-        roof = {'bound': 'mfma', 'kernel': 'riccati17_kernel', 'flop_per_stage': fl, 'achieved': ach,
-                'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak}
+        ex = None
+        pj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_full17.json')
+        if os.path.exists(pj) and args.dtype == 'f64' and B == 4096 and N == 60:
+            e = json.load(open(pj)).get('per_kernel', {}).get('mpcb::' + kname, {}).get('executed_flops_per_launch')
+            ex = e / (ph['riccati'] * 1e-3) / 1e12 / peak if e else None
+        roof = {'bound': 'valu', 'kernel': kname, 'flop_per_stage': fl, 'achieved': ach,
+                'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak, 'executed_frac': ex}
     print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
                       'unit': 'solves/s', 'ms_per_step': el / args.steps * 1e3, 'batch': B,
                       'dtype': args.dtype, 'bad_status': bad, 'bounds': args.bounds,

@@ -17,4 +17,8 @@ done
 timeout -k 10 200 python tools/bench_full17.py --dtype f32 --batch 16384 --steps 5 > $O/bench_full17_f32.log 2>&1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_full17 -o run -- \
   python3 tools/bench_full17.py --steps 5 > $O/stats_full17.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_full17_input -o run -- \
+  python3 tools/bench_full17.py --bounds input --steps 3 > $O/stats_full17_input.log 2>&1
+PROG=tools/bench_full17.py bash tools/profile_pmc.sh $O/pmc_full17 --bounds none --steps 2 --warmup 1
+python3 tools/pmc_summary.py $O/pmc_full17 --json $O/pmc_full17.json > $O/pmc_full17.txt
 echo round_end_done
