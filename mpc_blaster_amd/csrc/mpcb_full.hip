@@ -5,15 +5,18 @@
 // Three launches per chunk:
 //   nominal17  one thread per instance: the RK4 rollout of u_ref from x0 (or a copy of the
 //              persistent iterate) into the workspace;
-//   lin17ws    stage-parallel linearisation, 32 lanes per (instance, stage): lane j < 23
-//              integrates the RK4 tangent seeded with e_j, so column j of [A_k | B_k] lands in
-//              lane j (what acados' forward VDE computes); gaps in iterate mode;
-//   riccati17  32 lanes per instance (two per one-wave workgroup), lane j owning column j of the
-//              stage Hessian: the Riccati recursion over the cached [A|B] (P, [A|B] and the
-//              Hessian columns meet in LDS, the 6x6 input block is factorised redundantly per
-//              lane, P is symmetric by construction), then the forward pass (du = K dx + k on the
-//              input lanes, dx' = [A|B] (dx, du) + gap on the state lanes, exchanged through
-//              LDS) writing u0, X = xbar + dx, U = ubar + du and the status.
+//   lin17ws    stage-parallel linearisation, 16 lanes per (instance, stage): lanes 0..13
+//              integrate the RK4 tangents seeded with e_j of the 14 dense directions, so column j of
+//              [A_k | B_k] lands in a lane (what acados' forward VDE computes); lanes 14 / 15 write
+//              the 9 structural columns; gaps in iterate mode (lin17_packed, also behind
+//              mpcb_linearize);
+//   riccati    the Riccati pass, its forward pass and the interior point of the boxes:
+//              riccati17q_kernel (mpcb_r17.hip, 16 lanes per instance, the default) or, with
+//              MPCB_R17=0, riccati17_kernel below (32 lanes per instance, two per one-wave
+//              workgroup, lane j owning column j of the stage Hessian: P, [A|B] and the Hessian
+//              columns meet in LDS, the 6x6 input block is factorised redundantly per lane, P is
+//              symmetric by construction), each ending with the forward pass (du = K dx + k,
+//              dx' = [A|B] (dx, du) + gap) that writes u0, X = xbar + dx, U = ubar + du, status.
 // The 12/4 slice has its own MI355X-tuned kernels (mpcb_split.hip); this path carries the full
 // model at the reference's own dimensions and is not on the BASELINE benchmark configs.
 #include <hip/hip_runtime.h>
@@ -80,25 +83,47 @@ __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
   }
 }
 
-// ---- the linearisation of every interval, stage-parallel: 32 lanes per (instance, stage) -----
-// Lane j < 23 integrates the RK4 tangent seeded with e_j: column j of [A_k | B_k] (acados'
-// forward VDE).  LIN_WS: into the workspace (+ gaps, iterate mode); else into dense A / Bm.
-template <class T, bool LIN_WS>
-__device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>& M, const T* p,
-                                           int64_t p_sb, int64_t p_kb, const T* xbar, const T* ubar, int64_t b0,
-                                           T* ws, int mode, T* A, T* Bm, T* xnext) {
-  const int lane = threadIdx.x;
-  const int j = lane % L17;
-  const int64_t idx = (int64_t)blockIdx.x * G17 + lane / L17;   // (instance, stage) pair
-  if (idx >= B * N || j >= NZ17) return;
-  const int64_t c = idx / N;
-  const int k = (int)(idx % N);
-  const int64_t b = b0 + c;
+// ---- the linearisation of every interval, stage-parallel: 16 lanes per (instance, stage) -----
+constexpr int LQ17 = 16, GQ17 = 64 / LQ17;
+
+// One (instance, stage) of the packed linearisation, lane t < 16: column j of [A_k | B_k] into
+// col(j, v[17]) and, on lane 0, the RK4 successor into succ(xn[17]).  Shared by the workspace
+// kernel (lin17ws_kernel) and the dense debug export (linearize17_kernel, mpcb_linearize), so the
+// parity test of mpcb_linearize covers the arithmetic the solver runs.
+template <class T, class Col, class Succ>
+__device__ __forceinline__ void lin17_packed(int t, const T* pb, T h, const Model<T>& M, const T* xk,
+                                             const T* uk, Col&& colf, Succ&& succ) {
+  if (t >= 14) {
+    if (t == 14) {   // position and POC-state directions
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int jj = q < 3 ? q : 11 + q;
+        T v[NX17];
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) v[i] = (i == jj) ? T(1) : T(0);
+        colf(jj, v);
+      }
+    } else {         // velocity directions
+      P17<T> P;
+      unpack_p17(pb, P);
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        const int jj = 6 + cc;
+        T v[NX17];
+#pragma unroll
+        for (int i = 0; i < NX17; ++i) {
+          v[i] = (i == jj) ? T(1) : T(0);
+          if (i == cc) v[i] = h;
+          if (i >= 14) v[i] = h * P.Jp[(i - 14) * 3 + cc];
+        }
+        colf(jj, v);
+      }
+    }
+    return;
+  }
+  const int j = t < 3 ? 3 + t : (t < 8 ? 6 + t : 9 + t);   // 3..5, 9..13, 17..22
   P17<T> P;
-  unpack_p17(p + b * p_sb + k * p_kb, P);
-  const T* xk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)k * NX17 : xbar + (b * (N + 1) + k) * NX17;
-  const T* uk = LIN_WS ? ws + c * full17_elems(N) + (int64_t)(N + 1) * NX17 + (int64_t)k * NU17
-                       : ubar + (b * N + k) * NU17;
+  unpack_p17(pb, P);
   T x[NX17], u[NU17], dx[NX17], du[NU17], xn[NX17], col[NX17];
 #pragma unroll
   for (int i = 0; i < NX17; ++i) {
@@ -111,27 +136,8 @@ __device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>
     du[m] = (j == NX17 + m) ? T(1) : T(0);
   }
   rk4_17<T, true>(x, dx, u, du, h, M, P, xn, col);
-  if constexpr (LIN_WS) {
-    Ws17<T> w(ws + c * full17_elems(N), N);
-#pragma unroll
-    for (int i = 0; i < NX17; ++i) w.AB[((int64_t)k * NZ17 + j) * NX17 + i] = col[i];
-    if (j == 0) {   // gap Phi(xbar_k, ubar_k) - xbar_{k+1}; the rollout is gap-free by construction
-#pragma unroll
-      for (int i = 0; i < NX17; ++i)
-        w.GP[(int64_t)k * NX17 + i] = (mode == MPCB_MODE_ITERATE) ? xn[i] - xk[NX17 + i] : T(0);
-    }
-  } else {
-    const int64_t o = b * N + k;
-#pragma unroll
-    for (int i = 0; i < NX17; ++i) {
-      if (j < NX17) A[(o * NX17 + i) * NX17 + j] = col[i];
-      else Bm[(o * NX17 + i) * NU17 + (j - NX17)] = col[i];
-    }
-    if (j == 0 && xnext) {
-#pragma unroll
-      for (int i = 0; i < NX17; ++i) xnext[o * NX17 + i] = xn[i];
-    }
-  }
+  colf(j, col);
+  if (t == 0) succ(xn);
 }
 
 // The workspace linearisation packs 4 (instance, stage) pairs per wavefront, 16 lanes each:
@@ -139,7 +145,6 @@ __device__ __forceinline__ void lin17_body(int64_t B, int N, T h, const Model<T>
 // angles, the six inputs); lanes 14 / 15 write the 9 constant columns.  f does not depend on
 // the position or POC states (column e_j), and it is linear in the velocity with a constant
 // Jacobian (dk_1 = .. = dk_4 = c = e_pos + Jp e_v in the POC rows, so RK4 gives e_j + h c).
-constexpr int LQ17 = 16, GQ17 = 64 / LQ17;
 template <class T>
 __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
   const int lane = threadIdx.x;
@@ -153,55 +158,17 @@ __global__ void __launch_bounds__(64) lin17ws_kernel(FullArgs<T> a) {
   const T* pb = a.p ? a.p + b * a.p_sb + k * a.p_kb : a.W->p;
   Ws17<T> w(a.ws + c * full17_elems(N), N);
   T* ABk = w.AB + (int64_t)k * NZ17 * NX17;
-  if (t >= 14) {
-    if (t == 14) {   // position and POC-state directions
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int jj = q < 3 ? q : 11 + q;
-#pragma unroll
-        for (int i = 0; i < NX17; ++i) ABk[jj * NX17 + i] = (i == jj) ? T(1) : T(0);
-      }
-    } else {         // velocity directions
-      P17<T> P;
-      unpack_p17(pb, P);
-#pragma unroll
-      for (int cc = 0; cc < 3; ++cc) {
-        const int jj = 6 + cc;
-#pragma unroll
-        for (int i = 0; i < NX17; ++i) {
-          T v = (i == jj) ? T(1) : T(0);
-          if (i == cc) v = a.h;
-          if (i >= 14) v = a.h * P.Jp[(i - 14) * 3 + cc];
-          ABk[jj * NX17 + i] = v;
-        }
-      }
-    }
-    return;
-  }
-  const int j = t < 3 ? 3 + t : (t < 8 ? 6 + t : 9 + t);   // 3..5, 9..13, 17..22
-  P17<T> P;
-  unpack_p17(pb, P);
   const T* xk = w.XB + (int64_t)k * NX17;
-  const T* uk = w.UB + (int64_t)k * NU17;
-  T x[NX17], u[NU17], dx[NX17], du[NU17], xn[NX17], col[NX17];
+  lin17_packed<T>(t, pb, a.h, a.M, xk, w.UB + (int64_t)k * NU17,
+                  [&](int j, const T* v) {
 #pragma unroll
-  for (int i = 0; i < NX17; ++i) {
-    x[i] = xk[i];
-    dx[i] = (j == i) ? T(1) : T(0);
-  }
+                    for (int i = 0; i < NX17; ++i) ABk[j * NX17 + i] = v[i];
+                  },
+                  [&](const T* xn) {   // gap Phi(xbar_k, ubar_k) - xbar_{k+1}; the rollout is gap-free
 #pragma unroll
-  for (int m = 0; m < NU17; ++m) {
-    u[m] = uk[m];
-    du[m] = (j == NX17 + m) ? T(1) : T(0);
-  }
-  rk4_17<T, true>(x, dx, u, du, a.h, a.M, P, xn, col);
-#pragma unroll
-  for (int i = 0; i < NX17; ++i) ABk[j * NX17 + i] = col[i];
-  if (t == 0) {   // gap Phi(xbar_k, ubar_k) - xbar_{k+1}; the rollout is gap-free by construction
-#pragma unroll
-    for (int i = 0; i < NX17; ++i)
-      w.GP[(int64_t)k * NX17 + i] = (a.mode == MPCB_MODE_ITERATE) ? xn[i] - xk[NX17 + i] : T(0);
-  }
+                    for (int i = 0; i < NX17; ++i)
+                      w.GP[(int64_t)k * NX17 + i] = (a.mode == MPCB_MODE_ITERATE) ? xn[i] - xk[NX17 + i] : T(0);
+                  });
 }
 
 // ---- phases 1 + 2: Riccati backward over the cached [A|B], then the forward pass -------------
@@ -727,13 +694,33 @@ __global__ void __launch_bounds__(64) riccati17_kernel(FullArgs<T> a) {
   }
 }
 
-// [A|B] of every shooting interval into dense arrays (debug / parity, mpcb_linearize).
+// [A|B] of every shooting interval into dense arrays (debug / parity, mpcb_linearize), by the
+// solver's own packed linearisation (lin17_packed): 16 lanes per (instance, stage).
 template <class T>
 __global__ void __launch_bounds__(64) linearize17_kernel(int64_t B, int N, T h, Model<T> M,
                                                          const T* p, int64_t p_sb, int64_t p_kb,
                                                          const T* xbar, const T* ubar, T* A, T* Bm,
                                                          T* xnext) {
-  lin17_body<T, false>(B, N, h, M, p, p_sb, p_kb, xbar, ubar, 0, nullptr, 0, A, Bm, xnext);
+  const int lane = threadIdx.x;
+  const int t = lane % LQ17;
+  const int64_t o = (int64_t)blockIdx.x * GQ17 + lane / LQ17;   // (instance, stage) = b * N + k
+  if (o >= B * N) return;
+  const int64_t b = o / N;
+  const int k = (int)(o % N);
+  lin17_packed<T>(t, p + b * p_sb + k * p_kb, h, M, xbar + (b * (N + 1) + k) * NX17, ubar + o * NU17,
+                  [&](int j, const T* v) {
+#pragma unroll
+                    for (int i = 0; i < NX17; ++i) {
+                      if (j < NX17) A[(o * NX17 + i) * NX17 + j] = v[i];
+                      else Bm[(o * NX17 + i) * NU17 + (j - NX17)] = v[i];
+                    }
+                  },
+                  [&](const T* xn) {
+                    if (xnext) {
+#pragma unroll
+                      for (int i = 0; i < NX17; ++i) xnext[o * NX17 + i] = xn[i];
+                    }
+                  });
 }
 
 template <class T>
@@ -774,7 +761,7 @@ template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,
                               int64_t p_kb, const T* xbar, const T* ubar, T* A, T* Bm, T* xnext,
                               hipStream_t st) {
-  const unsigned grid = (unsigned)((B * N + G17 - 1) / G17);
+  const unsigned grid = (unsigned)((B * N + GQ17 - 1) / GQ17);
   hipLaunchKernelGGL(linearize17_kernel<T>, dim3(grid), dim3(64), 0, st, B, N, h, M, p, p_sb, p_kb, xbar,
                      ubar, A, Bm, xnext);
   return hipGetLastError();

@@ -114,6 +114,28 @@ def test_solve17_iterate_and_default_params_match_oracle():
     assert (m.get_status().cpu().numpy() == 0).all()
 
 
+@pytest.mark.parametrize('box', [False, True])
+def test_solve17_chunked_ragged_batches_match_oracle(box, monkeypatch):
+    """Several workspace chunks whose last wavefront is ragged (MPCB_CHUNK=64, B=150: chunks of
+    64, 64, 22 instances): the 16-lane kernel's extra groups run on private padding slots of the
+    workspace and must neither disturb the valid instances nor write outputs."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    monkeypatch.setenv('MPCB_CHUNK', '64')
+    N, B = 12, 150
+    kw = dict(lbu=LBU17, ubu=UBU17) if box else {}
+    m = BatchedMPC(MPCConfig.full(N=N, **kw), max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 404)
+    m.set_params(p)
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    o = mpc_solve17(x0, xref, uref, FullSpec(N=N, **kw), p)
+    tol = 1e-9 if not box else 1e-7
+    assert (m.get_status().cpu().numpy() == o['status']).all()
+    assert relerr(m.get_control().cpu().numpy(), o['u0']).max() <= tol
+    assert relerr(m.get_state_trajectory().cpu().numpy(), o['X']).max() <= tol
+    assert relerr(m.get_input_trajectory().cpu().numpy(), o['U']).max() <= tol
+
+
 def test_solve17_fp32_close_to_fp64_oracle():
     N, B = 20, 16
     m = _mpc(N, 'f32', max_batch=B)
