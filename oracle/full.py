@@ -16,8 +16,8 @@ parameters with T_blast = 21.582 at ``parameter_values[24]``):
   primal-dual interior point ``oracle.ocp.ipm_box_solve`` (acados uses HPIPM's interior point;
   the exact active set of the 12/4 path needs thousands of exchanges on this model).
 
-Not covered (the device path does not implement it either): the reference's state box
-(``idxbx``, stages 1..N-1) — see DESIGN.md.
+The reference's state box (``idxbx``, stages 1..N-1, ``FullSpec.lbx/ubx``) goes through the same
+interior point (explicit slacks with an infeasible start, ``oracle.ocp.ipm_box_solve``).
 """
 from __future__ import annotations
 
