@@ -612,14 +612,21 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     dxs = acc;
     dx8 = acc8;
     fin = fin && ((dxs - dxs) == T(0)) && ((dx8 - dx8) == T(0));
-    if (k + FD < N) load(k + FD, cr);   // refill this slot FD stages ahead
+    // refill this slot FD stages ahead, unconditionally (a clamped stage index past the end): a
+    // refill under a branch makes the count of loads in flight path-dependent, and the
+    // compiler then waits for every load (vmcnt(1)) at the top of each stage
+    load(k + FD < N ? k + FD : N - 1, cr);
     QSTAMP(1);
   };
-  for (int k0 = 0; k0 < N; k0 += FD) {
-    static_for<FD>([&](auto sl) {
-      if (k0 + decltype(sl)::value < N) stage(k0 + decltype(sl)::value, ring[decltype(sl)::value]);
-    });
+  // whole groups of FD stages without guards (a guarded stage makes the loads in flight
+  // path-dependent as well), then the N % FD remaining stages
+  int k0 = 0;
+  for (; k0 + FD <= N; k0 += FD) {
+    static_for<FD>([&](auto sl) { stage(k0 + decltype(sl)::value, ring[decltype(sl)::value]); });
   }
+  static_for<FD>([&](auto sl) {
+    if (k0 + decltype(sl)::value < N) stage(k0 + decltype(sl)::value, ring[decltype(sl)::value]);
+  });
   QSTAMP_DONE("fwd");
   if constexpr (STEP || !OUT) {
     T* base = STEP ? r.w.DDX : r.w.DX;
