@@ -48,17 +48,27 @@ __device__ __forceinline__ void unpack_p17(const T* __restrict__ p, P17<T>& P) {
   P.tb = p[24];
 }
 
-template <class T, bool TAN>
+// sin/cos of the five angles of f17 (Euler angles x[3..5], swivel angles x[12..13]), one thread
+struct Trig17Serial {
+  template <class T>
+  __device__ __forceinline__ void operator()(const T* __restrict__ x, T (&s)[5], T (&c)[5]) const {
+    sc(x[3], &s[0], &c[0]);
+    sc(x[4], &s[1], &c[1]);
+    sc(x[5], &s[2], &c[2]);
+    sc(x[12], &s[3], &c[3]);
+    sc(x[13], &s[4], &c[4]);
+  }
+};
+
+template <class T, bool TAN, class Trig = Trig17Serial>
 __device__ __forceinline__ void f17_tan(const T* __restrict__ x, const T* __restrict__ dx,
                                         const T* __restrict__ u, const T* __restrict__ du,
                                         const Model<T>& M, const P17<T>& P, T* __restrict__ f,
-                                        T* __restrict__ df) {
-  T sf, cf, st, ct, sp, cp, s1, c1, s2, c2;
-  sc(x[3], &sf, &cf);
-  sc(x[4], &st, &ct);
-  sc(x[5], &sp, &cp);
-  sc(x[12], &s1, &c1);
-  sc(x[13], &s2, &c2);
+                                        T* __restrict__ df, const Trig& trig = Trig()) {
+  T tsn[5], tcs[5];
+  trig(x, tsn, tcs);
+  const T sf = tsn[0], cf = tcs[0], st = tsn[1], ct = tcs[1], sp = tsn[2], cp = tcs[2];
+  const T s1 = tsn[3], c1 = tcs[3], s2 = tsn[4], c2 = tcs[4];
   const T ict = T(1) / ct;
   const T tt = st * ict;
   const T wx = x[9], wy = x[10], wz = x[11];
@@ -149,35 +159,35 @@ __device__ __forceinline__ void f17_tan(const T* __restrict__ x, const T* __rest
 }
 
 // One classic RK4 step (acados sim_erk: 4 stages, 1 step) of f17 with an optional tangent.
-template <class T, bool TAN>
+template <class T, bool TAN, class Trig = Trig17Serial>
 __device__ __forceinline__ void rk4_17(const T* __restrict__ x, const T* __restrict__ dx,
                                        const T* __restrict__ u, const T* __restrict__ du, T h,
                                        const Model<T>& M, const P17<T>& P, T* __restrict__ xn,
-                                       T* __restrict__ dxn) {
+                                       T* __restrict__ dxn, const Trig& trig = Trig()) {
   T k[NX17], dk[NX17], xs[NX17], dxs[NX17];
   const T h2 = T(0.5) * h, h6 = h / T(6);
-  f17_tan<T, TAN>(x, dx, u, du, M, P, k, dk);
+  f17_tan<T, TAN>(x, dx, u, du, M, P, k, dk, trig);
 #pragma unroll
   for (int i = 0; i < NX17; ++i) {
     xn[i] = k[i];
     xs[i] = x[i] + h2 * k[i];
     if constexpr (TAN) { dxn[i] = dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
   }
-  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk, trig);
 #pragma unroll
   for (int i = 0; i < NX17; ++i) {
     xn[i] += T(2) * k[i];
     xs[i] = x[i] + h2 * k[i];
     if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h2 * dk[i]; }
   }
-  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk, trig);
 #pragma unroll
   for (int i = 0; i < NX17; ++i) {
     xn[i] += T(2) * k[i];
     xs[i] = x[i] + h * k[i];
     if constexpr (TAN) { dxn[i] += T(2) * dk[i]; dxs[i] = dx[i] + h * dk[i]; }
   }
-  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk);
+  f17_tan<T, TAN>(xs, dxs, u, du, M, P, k, dk, trig);
 #pragma unroll
   for (int i = 0; i < NX17; ++i) {
     xn[i] = x[i] + h6 * (xn[i] + k[i]);

@@ -83,6 +83,86 @@ __global__ void __launch_bounds__(64) nominal17_kernel(FullArgs<T> a) {
   }
 }
 
+// The same rollout with 16 lanes per instance (4 instances per wavefront): the serial chain's
+// cost is the five sin/cos of every f evaluation, so lane t < 5 evaluates the pair of angle t and
+// a DPP row broadcast (v_mov_b32_dpp row_newbcast) hands the ten values to the row; the rest of
+// f17 runs redundantly in the 16 lanes (one instruction stream).  1024 wavefronts at B = 4096
+// instead of 64.
+template <int L> __device__ __forceinline__ float rowbc(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xF, 0xF, true));
+}
+template <int L> __device__ __forceinline__ double rowbc(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x150 + L, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x150 + L, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+struct Trig17Row {
+  int t;   // lane in the 16-lane row
+  template <class T>
+  __device__ __forceinline__ void operator()(const T* __restrict__ x, T (&sn)[5], T (&cs)[5]) const {
+    const uint64_t m1 = lane_mask(t == 1), m2 = lane_mask(t == 2), m3 = lane_mask(t == 3), m4 = lane_mask(t == 4);
+    T ang = csel(m1, x[4], x[3]);
+    ang = csel(m2, x[5], ang);
+    ang = csel(m3, x[12], ang);
+    ang = csel(m4, x[13], ang);
+    T s0, c0;
+    sc(ang, &s0, &c0);
+    sn[0] = rowbc<0>(s0); cs[0] = rowbc<0>(c0);
+    sn[1] = rowbc<1>(s0); cs[1] = rowbc<1>(c0);
+    sn[2] = rowbc<2>(s0); cs[2] = rowbc<2>(c0);
+    sn[3] = rowbc<3>(s0); cs[3] = rowbc<3>(c0);
+    sn[4] = rowbc<4>(s0); cs[4] = rowbc<4>(c0);
+  }
+};
+
+template <class T>
+__global__ void __launch_bounds__(64) nominal17q_kernel(FullArgs<T> a) {
+  const int lane = threadIdx.x;
+  const int t = lane & 15;
+  const int64_t c_raw = (int64_t)blockIdx.x * 4 + (lane >> 4);
+  const bool valid = c_raw < a.nb;
+  const int64_t c = valid ? c_raw : a.nb - 1;   // a ragged last wave recomputes the last instance
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  Ws17<T> w(a.ws + c * full17_elems(N), N);
+  if (a.mode == MPCB_MODE_ITERATE) {   // the persistent iterate (X/U may alias xbar/ubar: copy it first)
+    if (valid) {
+      for (int i = t; i < (N + 1) * NX17; i += 16) w.XB[i] = a.xbar[b * (int64_t)(N + 1) * NX17 + i];
+      for (int i = t; i < N * NU17; i += 16) w.UB[i] = a.ubar[b * (int64_t)N * NU17 + i];
+    }
+    return;
+  }
+  const bool wr = valid && t == 0;
+  P17<T> P;
+  const T* pb = a.p ? a.p + b * a.p_sb : a.W->p;
+  const int64_t pkb = a.p ? a.p_kb : 0;   // stage-varying parameters (acados set(k, 'p'))
+  unpack_p17(pb, P);
+  const T* ur = a.uref + b * a.uref_sb;
+  const Trig17Row trig{t};
+  T x[NX17], u[NU17];
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) {
+    x[i] = a.x0[b * a.x0_sb + i];
+    if (wr) w.XB[i] = x[i];
+  }
+  for (int k = 0; k < N; ++k) {
+#pragma unroll
+    for (int m = 0; m < NU17; ++m) {
+      u[m] = ur[(int64_t)k * NU17 + m];
+      if (wr) w.UB[(int64_t)k * NU17 + m] = u[m];
+    }
+    T xn[NX17];
+    if (pkb && k) unpack_p17(pb + k * pkb, P);
+    rk4_17<T, false>(x, nullptr, u, nullptr, a.h, a.M, P, xn, nullptr, trig);
+#pragma unroll
+    for (int i = 0; i < NX17; ++i) {
+      x[i] = xn[i];
+      if (wr) w.XB[(int64_t)(k + 1) * NX17 + i] = xn[i];
+    }
+  }
+}
+
 // ---- the linearisation of every interval, stage-parallel: 16 lanes per (instance, stage) -----
 constexpr int LQ17 = 16, GQ17 = 64 / LQ17;
 
@@ -135,7 +215,8 @@ __device__ __forceinline__ void lin17_packed(int t, const T* pb, T h, const Mode
     u[m] = uk[m];
     du[m] = (j == NX17 + m) ? T(1) : T(0);
   }
-  rk4_17<T, true>(x, dx, u, du, h, M, P, xn, col);
+  // the five sin/cos of the nominal point: lane t < 5 of the row evaluates one (Trig17Row)
+  rk4_17<T, true>(x, dx, u, du, h, M, P, xn, col, Trig17Row{t});
   colf(j, col);
   if (t == 0) succ(xn);
 }
@@ -742,7 +823,10 @@ __global__ void __launch_bounds__(64) sim17_kernel(int64_t B, T h, Model<T> M, c
 
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
+  if (a.q17)   // 16 lanes per instance (the lane-parallel trig); the thread-per-instance rollout otherwise
+    hipLaunchKernelGGL(nominal17q_kernel<T>, dim3((unsigned)((a.nb + 3) / 4)), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(nominal17_kernel<T>, dim3((unsigned)((a.nb + 63) / 64)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + GQ17 - 1) / GQ17)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
