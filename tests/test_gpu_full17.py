@@ -466,3 +466,26 @@ def test_set_t_blast_updates_default_parameter_in_place():
     p[24] = 15.0
     o = mpc_solve17(x0, xref, uref, FullSpec(N=N), p[None])
     assert relerr(m.get_control().cpu().numpy(), o['u0']).max() < 1e-9
+
+
+def test_full_size_17_input_box_properties():
+    """The reference OCP at its own horizon (N = 60) with the input box, 4096 instances (the
+    tools/bench_full17.py size): every status OK, every input inside the box, the interior point's
+    u0 equal to the oracle's on a sample of instances."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    N, B = 60, 4096
+    x0, xref, uref, p = _inputs(B, N, 2026)
+    m = BatchedMPC(MPCConfig.full(N=N, lbu=LBU17, ubu=UBU17), max_batch=B)
+    m.set_params(p)
+    m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    st = m.get_status().cpu().numpy()
+    U = m.get_input_trajectory().cpu().numpy()
+    assert (st == 0).all(), np.bincount(st)
+    assert (U >= LBU17 - 1e-9).all() and (U <= UBU17 + 1e-9).all()
+    idx = np.arange(0, B, 257)
+    o = mpc_solve17(x0[idx], xref[idx], uref[idx], FullSpec(N=N, lbu=LBU17, ubu=UBU17), p[idx])
+    assert (o['status'] == 0).all()
+    e = relerr(m.get_control().cpu().numpy()[idx], o['u0']).max()
+    print(f'17/6 input box N=60 B=4096: sampled u0 vs oracle {e:.2e}, oracle iterations max {o["iters"].max()}')
+    assert e <= 1e-7
