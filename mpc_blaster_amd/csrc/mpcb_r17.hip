@@ -257,6 +257,7 @@ __device__ __forceinline__ void prefetch(const Ctx<T>& r, int k, Pre<T>& p) {
 template <class T>
 struct Cur {
   T dxs, dx8, du, ll, lu;               // dx_k[s], dx_k[8], (du, lambda_l, lambda_u)_k[m]
+  T ddxs, ddx8;                         // the last Newton step of dx_k[s], dx_k[8] (pending)
   T ixs[4], ix8[4];                     // state rows (s_l, s_u, lambda_l, lambda_u) of s and 8
 };
 template <class T>
@@ -264,6 +265,8 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
   const int64_t kx = (int64_t)k * NX17;
   p.dxs = r.w.DX[kx + r.s];
   p.dx8 = r.w.DX[kx + OM];
+  p.ddxs = r.w.DDX[kx + r.s];
+  p.ddx8 = r.w.DDX[kx + OM];
   const T* ip = r.w.IP + (int64_t)k * 18;
   p.du = ip[r.m];
   p.ll = ip[6 + r.m];
@@ -277,9 +280,11 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
 }
 
 // Riccati backward over the cached [A|B] (+ gaps in iterate mode, + the interior point's barrier
-// terms and the iterate shift when r.a.box).  Writes K (row-major 6 x 17) and k to KR.
+// terms and the iterate shift when r.a.box).  Writes K (row-major 6 x 17) and k to KR.  With the
+// box, the previous iteration's step of the state trajectory, dx += apend ddx, is applied here
+// stage by stage (written back to DX) instead of in a pass of its own.
 template <class T>
-__device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
+__device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0)) {
   const FullArgs<T>& a = r.a;
   const bool ipm = a.box != 0;
   const bool gaps = !ipm && a.mode == MPCB_MODE_ITERATE;
@@ -295,8 +300,15 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
   {
     T xs = r.w.XB[(int64_t)N * NX17 + s], x8 = r.w.XB[(int64_t)N * NX17 + OM];
     if (ipm) {
-      xs += r.w.DX[(int64_t)N * NX17 + s];
-      x8 += r.w.DX[(int64_t)N * NX17 + OM];
+      T* dxn = r.w.DX + (int64_t)N * NX17;
+      const T* ddn = r.w.DDX + (int64_t)N * NX17;
+      // (a select, not a product with apend = 0: DDX is not yet written before the first step)
+      const T ys = (apend != T(0)) ? dxn[s] + apend * ddn[s] : dxn[s];
+      const T y8 = (apend != T(0)) ? dxn[OM] + apend * ddn[OM] : dxn[OM];
+      dxn[s] = ys;
+      dxn[OM] = y8;
+      xs += ys;
+      x8 += y8;
     }
     L.V[s] = xs - r.xr[(int64_t)N * NX17 + s];
     L.V[OM] = x8 - r.xr[(int64_t)N * NX17 + OM];
@@ -358,6 +370,12 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) g8 += cu.a8[q] * y[c8row(q)];
     QSTAMP(2);
+    if (ipm) {   // the pending step of this stage's iterate (unconditional stores)
+      ic.dxs = (apend != T(0)) ? ic.dxs + apend * ic.ddxs : ic.dxs;
+      ic.dx8 = (apend != T(0)) ? ic.dx8 + apend * ic.ddx8 : ic.dx8;
+      r.w.DX[(int64_t)k * NX17 + s] = ic.dxs;
+      r.w.DX[(int64_t)k * NX17 + OM] = ic.dx8;
+    }
     // cost residual (ybar [+ iterate] - yref) into LDS (general Q, R)
     L.V[s] = (ipm ? cu.xs + ic.dxs : cu.xs) - cu.xrs;
     L.V[OM] = (ipm ? cu.x8 + ic.dx8 : cu.x8) - cu.xr8;
@@ -719,14 +737,27 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     bool done = false;
     T prev_alpha = T(1);
     int nshort = 0;
+    T mu = T(0), res = T(0);       // duality measure, state-row residual (of the current iterate)
+    T part_n = T(0), res_n = T(0); // their partial sums over the lane's rows after an update
+    T apend = T(0);                // the last step length, not yet applied to DX
     constexpr bool F64 = sizeof(T) == 8;
     const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
     const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
     QSTAMP_INIT();
     for (int it = 0; it < a.max_as_iter; ++it) {
       QSTAMP(6);
-      // duality measure mu = mean(lambda s), primal residual of the state rows
-      T part = T(0), res = T(0);
+      // duality measure mu = mean(lambda s), primal residual of the state rows: a pass over the
+      // rows at the start, afterwards summed by the update pass of the previous iteration (same
+      // rows, same order, same arithmetic); an instance that did not move keeps its values
+      if (it > 0) {
+        const T mu_n = row_sum(part_n) / (T(2) * rows), res_nr = row_max(res_n);
+        if (apend != T(0)) {
+          mu = mu_n;
+          res = sbox ? res_nr : T(0);
+        }
+      } else {
+      T part = T(0);
+      res = T(0);
       if (in) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
@@ -745,14 +776,17 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         for (int k = 1; k < N; ++k) acc_row(k, s);
         for (int k = 1 + t; k < N; k += LN) acc_row(k, OM);
       }
-      const T mu = row_sum(part) / (T(2) * rows);
+      mu = row_sum(part) / (T(2) * rows);
       if (sbox) res = row_max(res);
+      }
       done = done || (!(mu > ipm_tol) && !(res > ipm_res));
       if (__all(done || !valid)) break;
       QSTAMP(0);
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
       const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
-      if (!backward<T>(r, smu) && !done) {
+      const bool ok_b = backward<T>(r, smu, apend);
+      apend = T(0);
+      if (!ok_b && !done) {
         // a Newton system that lost positive definiteness near the solution: keep the current
         // iterate as converged; earlier it is a failure
         if (!(mu > ipm_brk) && !(res > ipm_res)) done = true;
@@ -816,6 +850,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
         done = true;
       }
+      part_n = T(0);
+      res_n = T(0);
       if (!done && valid && in) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
@@ -825,9 +861,11 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
           const T ll = ip[6 + m], lu = ip[12 + m];
           const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
-          ip[m] += alpha * d;
-          ip[6 + m] = ll + alpha * dll;
-          ip[12 + m] = lu + alpha * dlu;
+          const T dun = ip[m] + alpha * d, lln = ll + alpha * dll, lun = lu + alpha * dlu;
+          ip[m] = dun;
+          ip[6 + m] = lln;
+          ip[12 + m] = lun;
+          part_n += lln * (dun - (lbm - ubk)) + lun * ((ubm - ubk) - dun);
         }
       }
       if (!done && valid && sbox) {   // state-row slacks and multipliers (before DX moves)
@@ -838,10 +876,20 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
           const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
           T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
-          ix[0] = sr.sl + alpha * dsl;
-          ix[NX17] = sr.su + alpha * dsu;
-          ix[2 * NX17] = sr.ll + alpha * dll;
-          ix[3 * NX17] = sr.lu + alpha * dlu;
+          SRow<T> nr = sr;   // the row after the step (dx moves by alpha ddx in the next backward)
+          nr.y = sr.y + alpha * dy;
+          nr.sl = sr.sl + alpha * dsl;
+          nr.su = sr.su + alpha * dsu;
+          nr.ll = sr.ll + alpha * dll;
+          nr.lu = sr.lu + alpha * dlu;
+          nr.rl = nr.y - nr.lb - nr.sl;
+          nr.ru = nr.ub - nr.y - nr.su;
+          ix[0] = nr.sl;
+          ix[NX17] = nr.su;
+          ix[2 * NX17] = nr.ll;
+          ix[3 * NX17] = nr.lu;
+          part_n += nr.ll * nr.sl + nr.lu * nr.su;
+          res_n = fmax(res_n, fmax(fabs(nr.rl), fabs(nr.ru)));
         };
 #pragma unroll 4
         for (int k = 1; k < N; ++k) upd_row(k, s);
@@ -849,19 +897,19 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       }
       __syncthreads();   // the rows of state 8 are read by every lane of the next backward
       QSTAMP(4);
-      if (!done && valid) {
-        for (int k = 0; k <= N; ++k) r.w.DX[(int64_t)k * NX17 + s] += alpha * r.w.DDX[(int64_t)k * NX17 + s];
-        for (int k = t; k <= N; k += LN) r.w.DX[(int64_t)k * NX17 + OM] += alpha * r.w.DDX[(int64_t)k * NX17 + OM];
-      }
-      __syncthreads();
+      apend = (!done && valid) ? alpha : T(0);
     }
     QSTAMP(5);
     QSTAMP_DONE("ipm");
     if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
     // outputs: X = xbar + dx, U = ubar + du of the final iterate
     fin = true;
-    for (int k = 0; k <= N; ++k) {
-      const T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
+    for (int k = 0; k <= N; ++k) {   // (with the last step, when it is still pending)
+      T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
+      if (apend != T(0)) {
+        xs = xs + apend * r.w.DDX[(int64_t)k * NX17 + s];
+        x8 = x8 + apend * r.w.DDX[(int64_t)k * NX17 + OM];
+      }
       if (valid && a.X) {
         T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
         xo[s] = r.w.XB[(int64_t)k * NX17 + s] + xs;
