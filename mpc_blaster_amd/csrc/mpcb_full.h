@@ -299,7 +299,7 @@ struct Ws17 {
 
 constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
 // (IPM17_BREAK: oracle.ocp.IPM_BREAK_TOL, where the choice of 1e-6 is explained)
-constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-6, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
+constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-5, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
 constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
 constexpr int IPM17_SHORT_RUN = 10;
 // fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit
