@@ -34,6 +34,9 @@
 
 // forward-pass ring depths (stages of row loads in flight): the unconstrained pass, the interior
 // point's Newton-step pass
+#ifndef MPCB_Q17_ROWS_UNROLL   // stages per group of the interior point's row passes (loads in flight)
+#define MPCB_Q17_ROWS_UNROLL 4
+#endif
 #ifndef MPCB_Q17_FD
 #define MPCB_Q17_FD 3
 #endif
@@ -759,7 +762,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       T part = T(0);
       res = T(0);
       if (in) {
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           const T* ip = r.w.IP + (int64_t)k * 18;
@@ -772,7 +775,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           part += sr.ll * sr.sl + sr.lu * sr.su;
           res = fmax(res, fmax(fabs(sr.rl), fabs(sr.ru)));
         };
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 1; k < N; ++k) acc_row(k, s);
         for (int k = 1 + t; k < N; k += LN) acc_row(k, OM);
       }
@@ -801,7 +804,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       T amax = T(1) / T(IPM17_TAU);
       bool dfin = true;   // a finite direction from strictly positive slacks
       if (in) {
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           const T* ip = r.w.IP + (int64_t)k * 18;
@@ -829,7 +832,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
           if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
         };
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 1; k < N; ++k) step_row(k, s);
         for (int k = 1 + t; k < N; k += LN) step_row(k, OM);
       }
@@ -853,7 +856,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       part_n = T(0);
       res_n = T(0);
       if (!done && valid && in) {
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           T* ip = r.w.IP + (int64_t)k * 18;
@@ -891,7 +894,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           part_n += nr.ll * nr.sl + nr.lu * nr.su;
           res_n = fmax(res_n, fmax(fabs(nr.rl), fabs(nr.ru)));
         };
-#pragma unroll 4
+#pragma unroll MPCB_Q17_ROWS_UNROLL
         for (int k = 1; k < N; ++k) upd_row(k, s);
         for (int k = 1 + t; k < N; k += LN) upd_row(k, OM);
       }
