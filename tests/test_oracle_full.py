@@ -158,3 +158,30 @@ def test_ipm_state_box_kkt():
     stat, viol, gap = dense_kkt_certificate(o['A'], o['B'], o['gap'], np.zeros((B, 17)), o['xbar'], o['ubar'],
                                             xref, uref, spec, du, lbx=lbx, ubx=ubx)
     assert stat.max() <= 1e-9 and viol.max() <= 1e-9 and gap.max() <= 1e-8, (stat, viol, gap)
+
+
+def test_ipm_state_box_thin_interior_instances_converge():
+    """The two LP-feasible bench instances whose Newton system breaks before mu = 1e-8
+    (tests/golden/sbox_thin_interior.npz): the oracle keeps the iterate at the breakdown as
+    converged (IPM_BREAK_TOL, oracle/ocp.py) and its U carries a KKT certificate of the condensed
+    QP; an LP says both QPs are feasible."""
+    from oracle.ocp import IPM_BREAK_TOL, dense_kkt_certificate, lp_box_feasible
+    d = np.load(os.path.join(GOLD, 'sbox_thin_interior.npz'))
+    lbx, ubx, x0, p = d['lbx'], d['ubx'], d['x0'], d['p']
+    N, B = int(d['N']), x0.shape[0]
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2], xref[..., 14] = 3.5, 0.2
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    lbu = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])
+    ubu = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+    spec = FullSpec(N=N, lbu=lbu, ubu=ubu, lbx=lbx, ubx=ubx)
+    with np.errstate(all='ignore'):
+        o = mpc_solve17(x0, xref, uref, spec, p)
+    assert IPM_BREAK_TOL >= 1e-5
+    assert (o['status'] == 0).all(), o['status']
+    dx0 = x0 - o['xbar'][:, 0]
+    assert lp_box_feasible(o['A'], o['B'], o['gap'], dx0, o['xbar'], o['ubar'], spec, lbx, ubx).all()
+    stat, viol, gap = dense_kkt_certificate(o['A'], o['B'], o['gap'], dx0, o['xbar'], o['ubar'], xref, uref, spec,
+                                            o['U'] - o['ubar'], lbx=lbx, ubx=ubx)
+    assert stat.max() <= 1e-6 and viol.max() <= 1e-9 and gap.max() <= 1e-4
