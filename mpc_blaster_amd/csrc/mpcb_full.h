@@ -229,9 +229,10 @@ struct FullArgs {
 
 __host__ __device__ constexpr int64_t full17_elems(int N) {
   // XB (N+1)x17 | UB Nx6 | AB N x 23 columns x 17 | KR N x (6x17 + 6) | GP N x 17 |
-  // boxes: DX, DDX (N+1)x17 | IP N x 18 | DDU N x 6 | IX (N+1) x 4 x 17
+  // boxes: DX, DDX (N+1)x17 | IP N x 18 | DDU N x 6 | IX (N+1) x 4 x 17 | LC N x 24 | DAX (N+1)x17 | DAU N x 6 | DC N x 48 | GV (N+1) x 24
   return (int64_t)(N + 1) * NX17 + (int64_t)N * (NU17 + NZ17 * NX17 + NU17 * NX17 + NU17 + NX17) +
-         2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17) + 4 * (int64_t)(N + 1) * NX17;
+         2 * (int64_t)(N + 1) * NX17 + (int64_t)N * (18 + NU17) + 4 * (int64_t)(N + 1) * NX17 +
+         (int64_t)N * 24 + (int64_t)(N + 1) * NX17 + (int64_t)N * NU17 + (int64_t)N * 48 + (int64_t)(N + 1) * 24;
 }
 
 // n x n Cholesky (row-major H, lower L with 1/L_ii on the diagonal) and the solve L L^T x = b
@@ -294,6 +295,25 @@ struct Ws17 {
     DDU = IP + (int64_t)N * 18;                  // [N][6]
     // state box: slacks and multipliers s_l | s_u | lambda_l | lambda_u of the rows of stage k
     IX = DDU + (int64_t)N * NU17;                // [N+1][4][17]
+  }
+};
+
+// The Mehrotra arrays after IX (mpcb_r17.hip; a separate carve so the other 17/6 kernels keep
+// their register footprint): the packed Cholesky factor of Huu per stage (21 of 24), the
+// predictor's (affine) direction, and per row (z index: states, then 17 + m) w = 1/s_l - 1/s_u at
+// [0, 24), c = Delta s_a Delta lambda_a / s_l - (upper) at [24, 48): the corrector's gradient
+// change is c - sigma mu w.  GV: the predictor's stage gradients without the p terms (cost and
+// barrier: states at [0, 17), inputs at [17, 23)), and p_N at stage N.
+template <class T>
+struct WsM17 {
+  T *LC, *DAX, *DAU, *DC, *GV;
+  static constexpr int LC_N = 24, DC_N = 48;
+  __device__ __forceinline__ WsM17(const Ws17<T>& w, int N) {
+    LC = w.IX + (int64_t)(N + 1) * 4 * NX17;     // [N][24]
+    DAX = LC + (int64_t)N * LC_N;                // [N+1][17]
+    DAU = DAX + (int64_t)(N + 1) * NX17;         // [N][6]
+    DC = DAU + (int64_t)N * NU17;                // [N][48]
+    GV = DC + (int64_t)N * DC_N;                 // [N+1][24]
   }
 };
 

@@ -34,9 +34,6 @@
 
 // forward-pass ring depths (stages of row loads in flight): the unconstrained pass, the interior
 // point's Newton-step pass
-#ifndef MPCB_Q17_ROWS_UNROLL   // stages per group of the interior point's row passes (loads in flight)
-#define MPCB_Q17_ROWS_UNROLL 4
-#endif
 #ifndef MPCB_Q17_FD
 #define MPCB_Q17_FD 3
 #endif
@@ -201,6 +198,7 @@ template <class T>
 struct Ctx {
   const FullArgs<T>& a;
   Ws17<T> w;
+  WsM17<T> wm;        // Mehrotra arrays (riccati17q_kernel<T, true, true>)
   const T* xr;
   const T* ur;
   Lds<T>& L;
@@ -286,7 +284,7 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
 // terms and the iterate shift when r.a.box).  Writes K (row-major 6 x 17) and k to KR.  With the
 // box, the previous iteration's step of the state trajectory, dx += apend ddx, is applied here
 // stage by stage (written back to DX) instead of in a pass of its own.
-template <class T>
+template <class T, bool MEH = false>
 __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0)) {
   const FullArgs<T>& a = r.a;
   const bool ipm = a.box != 0;
@@ -327,6 +325,11 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
     }
     P88 = W.QN[OM * NX17 + OM];
     wave_lds_sync();
+    if constexpr (MEH) {   // p_N for the corrector's vector pass
+      T* gv = r.wm.GV + (int64_t)N * 24;
+      gv[s] = pj;
+      gv[OM] = p8;
+    }
   }
   // box constants in registers (a load consumed on the spot would wait inside the stage loop)
   const T lbm = W.lbu[r.m], ubm = W.ubu[r.m];
@@ -388,14 +391,21 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
     for (int ci = 0; ci < 6; ++ci) L.YC[ci][t] = y[ids(ci)];
     wave_lds_sync();
     // ---- input lanes: their column G[:, 17+m] (+ s R, + barrier) -> Huu, h_u, Hux[:, 8]
+    T gu_own = T(0);   // (MEH) the input's gradient without the p term
     if (in) {
       const int m = r.m;
       T hu = hab;
+      T gu = T(0);
 #pragma unroll
       for (int n = 0; n < NU17; ++n) {
         const T wr = r.sR[n * NU17 + m];
-        hu += wr * L.V[NX17 + n];
+        if constexpr (MEH) gu += wr * L.V[NX17 + n];
+        else hu += wr * L.V[NX17 + n];
         L.HU[m][n] = g[8 + n] + wr;
+      }
+      if constexpr (MEH) {
+        gu_own = gu;
+        hu = hab + gu;
       }
       if (ipm) {
         const T sl = ic.du - (lbm - cu.ub), su = (ubm - cu.ub) - ic.du;
@@ -423,12 +433,15 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
       Gs[OM] = csel(m_in, spc, g8);
     }
     T hs = in ? pt : hab;   // AB[:, c]^T pt = pt_c for an identity state
+    T gs = T(0);            // (MEH) the state's gradient without the p term
 #pragma unroll
     for (int i = 0; i < NX17; ++i) {
       const T wq = r.sQ[i * NX17 + s];
       Gs[i] += wq;
-      hs += wq * L.V[i];
+      if constexpr (MEH) gs += wq * L.V[i];
+      else hs += wq * L.V[i];
     }
+    if constexpr (MEH) hs = hs + gs;
     // row 8 of every lane's G column is needed as the distributed column 8 of G; G[8,8] itself:
     // a^T P a with a = AB[:, 8] (rows 8, 2, 14..16) from P88, the lanes' P[8, .] and (P a)
     T spc_own = T(0);
@@ -444,8 +457,19 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
             cu.a8[3] * bcast<tstate(15)>(spc_own) + cu.a8[4] * bcast<tstate(16)>(spc_own);
       h8 = cu.a8[0] * pt8 + cu.a8[1] * bcast<tstate(2)>(pt) + cu.a8[2] * bcast<tstate(14)>(pt) +
            cu.a8[3] * bcast<tstate(15)>(pt) + cu.a8[4] * bcast<tstate(16)>(pt);
+      T gr8 = T(0);
 #pragma unroll
-      for (int i = 0; i < NX17; ++i) h8 += r.sQ[OM * NX17 + i] * L.V[i];
+      for (int i = 0; i < NX17; ++i) {
+        if constexpr (MEH) gr8 += r.sQ[OM * NX17 + i] * L.V[i];
+        else h8 += r.sQ[OM * NX17 + i] * L.V[i];
+      }
+      if constexpr (MEH) {   // (no state rows in the Mehrotra kernel: the gradients are complete)
+        h8 = h8 + gr8;
+        T* gv = r.wm.GV + (int64_t)k * 24;
+        gv[s] = gs;
+        gv[OM] = gr8;
+        gv[in ? NX17 + r.m : 23] = gu_own;
+      }
       G88 += r.sQ[OM * NX17 + OM];
     }
     if (sbox && k > 0) {   // state-box rows of this stage: barrier terms on the state diagonals
@@ -470,6 +494,16 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
     }
     T Lc[NU17 * NU17];
     chol_n<T, NU17>(H, Lc);
+    if constexpr (MEH) {   // packed lower triangle (row i at i(i+1)/2): lane t stores entries t and 16 + t % 5
+      T pk[21];
+#pragma unroll
+      for (int i = 0; i < NU17; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) pk[i * (i + 1) / 2 + j] = Lc[i * NU17 + j];
+      T* lc = r.wm.LC + (int64_t)k * WsM17<T>::LC_N;
+      lc[t] = sel<16>(pk, t);
+      lc[16 + t % 5] = sel<5>(pk + 16, t % 5);
+    }
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < NU17; ++i) ok = ok && (Lc[i * NU17 + i] == Lc[i * NU17 + i]);
@@ -542,6 +576,110 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
   }
   QSTAMP_DONE("bwd");
   return qp_ok;
+}
+
+// Mehrotra's corrector: its LQ problem has the predictor's matrices (same iterate, same D) and a
+// gradient that differs only by the rows' target terms
+//   Delta d = -(t_l/s_l - t_u/s_u),  t = sigma mu - Delta s_a Delta lambda_a,   = c - sigma mu w
+// (w, c per row in DC).  This pass is the vector half of the Riccati recursion for the corrector's
+// gradient (the predictor's stage gradients without the p terms in GV, plus Delta d) over the
+// stored factor (LC) and gains (KR):
+//   h_u = B^T p + g_u + Delta d_u,   k = -Huu^{-1} h_u,   p' = A^T p + g_x + Delta d_x + K^T h_u
+// (K^T h_u = Hxu k), from p_N, and overwrites k.  (The full gradient, not the difference alone:
+// near the conditioning limit, lambda / s ~ 1e16, predictor k + correction k cancelled to ~1e-6.)
+// Uniform stage values (the factor, K's column of state 8) are loaded spread over the lanes and
+// taken by row broadcasts.
+template <class T>
+struct PreC {
+  T ab[NX17];      // column z of [A_k | B_k]
+  T a8[5];         // the nonzeros of column 8
+  T ks[NU17];      // K[:, s]
+  T k8;            // K[t % 6, 8]
+  T gs, g8, gu;    // the predictor's gradients without the p terms
+  T lc0, lc1;      // packed factor entries t and 16 + t % 5
+  T ws, cs, w8, c8, wu, cu;
+};
+
+template <class T>
+__device__ __forceinline__ void prefetch_c(const Ctx<T>& r, int k, PreC<T>& p) {
+  const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
+#pragma unroll
+  for (int i = 0; i < NX17; ++i) p.ab[i] = ABk[r.z * NX17 + i];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) p.a8[q] = ABk[OM * NX17 + c8row(q)];
+  const T* kr = r.w.KR + (int64_t)k * Ws17<T>::KR_N;
+#pragma unroll
+  for (int n = 0; n < NU17; ++n) p.ks[n] = kr[n * NX17 + r.s];
+  p.k8 = kr[(r.t % NU17) * NX17 + OM];
+  const T* gv = r.wm.GV + (int64_t)k * 24;
+  p.gs = gv[r.s];
+  p.g8 = gv[OM];
+  p.gu = gv[NX17 + r.m];
+  const T* lc = r.wm.LC + (int64_t)k * WsM17<T>::LC_N;
+  p.lc0 = lc[r.t];
+  p.lc1 = lc[16 + r.t % 5];
+  const T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
+  p.ws = dc[r.s];
+  p.cs = dc[24 + r.s];
+  p.w8 = dc[OM];
+  p.c8 = dc[24 + OM];
+  p.wu = dc[NX17 + r.m];
+  p.cu = dc[24 + NX17 + r.m];
+}
+
+template <class T>
+__device__ __forceinline__ void backward_corr(const Ctx<T>& r, T smu) {
+  const int s = r.s, N = r.a.N;
+  const bool in = r.in;
+  T pc = r.wm.GV[(int64_t)N * 24 + s], pc8 = r.wm.GV[(int64_t)N * 24 + OM];
+  PreC<T> nx;
+  prefetch_c(r, N - 1, nx);
+  for (int k = N - 1; k >= 0; --k) {
+    const PreC<T> cu = nx;
+    prefetch_c(r, k > 0 ? k - 1 : 0, nx);
+    // [A|B]_z^T p (B^T p at input m on the input lanes)
+    T hab = pc8 * cu.ab[OM];
+    static_for<LN>([&](auto l) {
+      constexpr int tl = decltype(l)::value;
+      hab += bcast<tl>(pc) * cu.ab[sown(tl)];
+    });
+    const T hu = hab + cu.gu + (cu.cu - smu * cu.wu);
+    T h6[NU17];
+    static_for<NU17>([&](auto n) { h6[decltype(n)::value] = bcast<8 + decltype(n)::value>(hu); });
+    const T hs = (in ? pc : hab) + cu.gs + (cu.cs - smu * cu.ws);
+    const T h8 = cu.a8[0] * pc8 + cu.a8[1] * bcast<tstate(2)>(pc) + cu.a8[2] * bcast<tstate(14)>(pc) +
+                 cu.a8[3] * bcast<tstate(15)>(pc) + cu.a8[4] * bcast<tstate(16)>(pc) + cu.g8 + (cu.c8 - smu * cu.w8);
+    // the factor from the lanes' packed entries
+    T Lc[NU17 * NU17];
+    static_for<21>([&](auto pp) {
+      constexpr int p_ = decltype(pp)::value;
+      constexpr int i = p_ < 1 ? 0 : p_ < 3 ? 1 : p_ < 6 ? 2 : p_ < 10 ? 3 : p_ < 15 ? 4 : 5;
+      constexpr int j = p_ - i * (i + 1) / 2;
+      if constexpr (p_ < 16) Lc[i * NU17 + j] = bcast<p_>(cu.lc0);
+      else Lc[i * NU17 + j] = bcast<p_ - 16>(cu.lc1);
+    });
+    T nb[NU17], kc[NU17];
+#pragma unroll
+    for (int n = 0; n < NU17; ++n) nb[n] = -h6[n];
+    chol_n_solve<T, NU17>(Lc, nb, kc);
+    r.w.KR[(int64_t)k * Ws17<T>::KR_N + NU17 * NX17 + r.m] = sel<NU17>(kc, r.m);
+    T pn = hs, pn8 = h8;
+    static_for<NU17>([&](auto n) {
+      constexpr int n_ = decltype(n)::value;
+      pn += cu.ks[n_] * h6[n_];
+      pn8 += bcast<n_>(cu.k8) * h6[n_];
+    });
+    pc = pn;
+    pc8 = pn8;
+  }
+}
+
+// complementarity targets of a row for Mehrotra's corrector: t = sigma mu - Delta s_a Delta lambda_a
+template <class T>
+__device__ __forceinline__ void targets(T smu, T sl, T su, T ll, T lu, T dsl_a, T dsu_a, T& tl, T& tu) {
+  const T dll_a = (-ll * sl - ll * dsl_a) / sl, dlu_a = (-lu * su - lu * dsu_a) / su;
+  tl = smu - dsl_a * dll_a;
+  tu = smu - dsu_a * dlu_a;
 }
 
 // Forward pass over K, k.  GAIN: du = K dx + k; else du from the interior point's iterate (the
@@ -668,7 +806,9 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
 // The interior point of mpcb_full.hip riccati17_kernel<T, true> (same iteration as
 // oracle.ocp.ipm_box_solve) in this layout: input rows owned by the input lanes, state rows by the
 // owner of the state, the rows of state 8 spread over the lanes by stage (k = 1 + t, 1 + t + 16 ..).
-template <class T, bool BOX>
+// MEH (fp64, the input box alone): Mehrotra's predictor-corrector (oracle.ocp._ipm_box_mehrotra)
+// instead of the adaptive centring.
+template <class T, bool BOX, bool MEH>
 __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   __shared__ Lds<T> lds_all[GR];
   __shared__ T sQ[NX17 * NX17];
@@ -692,7 +832,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   for (int e = lane; e < NX17 * NX17; e += 64) sQ[e] = a.s * W.Q[e];
   for (int e = lane; e < NU17 * NU17; e += 64) sR[e] = a.s * W.R[e];
   __syncthreads();
-  const Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
+  const Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), WsM17<T>(Ws17<T>(a.ws + c * full17_elems(N), N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
                  lds_all[q], sQ, sR, t, s, zcol(t), m, in, valid};
   Lds<T>& L = r.L;
   const T* x0 = a.x0 + b * a.x0_sb;
@@ -720,7 +860,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     __syncthreads();
     forward<T, false, false, false>(r, dx0s, dx08, false);   // DX of the starting point
     __syncthreads();
-    const bool sbox = a.sbox != 0;
+    const bool sbox = !MEH && a.sbox != 0;
     // state rows: s = max(distance to the bound, theta w), lambda = 1
     auto srow_init = [&](int k, int i) {
       const T xb = r.w.XB[(int64_t)k * NX17 + i], y = r.w.DX[(int64_t)k * NX17 + i];
@@ -762,7 +902,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       T part = T(0);
       res = T(0);
       if (in) {
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           const T* ip = r.w.IP + (int64_t)k * 18;
@@ -775,7 +915,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           part += sr.ll * sr.sl + sr.lu * sr.su;
           res = fmax(res, fmax(fabs(sr.rl), fabs(sr.ru)));
         };
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 1; k < N; ++k) acc_row(k, s);
         for (int k = 1 + t; k < N; k += LN) acc_row(k, OM);
       }
@@ -785,8 +925,10 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       done = done || (!(mu > ipm_tol) && !(res > ipm_res));
       if (__all(done || !valid)) break;
       QSTAMP(0);
+      T smu;
+      if constexpr (!MEH) {
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
-      const T smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
+      smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
       const bool ok_b = backward<T>(r, smu, apend);
       apend = T(0);
       if (!ok_b && !done) {
@@ -800,18 +942,93 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       forward<T, true, true, false>(r, T(0), T(0), false);   // the Newton step -> DDX, DDU
       __syncthreads();
       QSTAMP(2);
+      } else {
+      // predictor: targets 0 -> the affine direction into DAX / DAU (K, k, the factor of Huu and
+      // the stage gradients stay in KR / LC / GV)
+      const bool ok_b = backward<T, true>(r, T(0), apend);
+      apend = T(0);
+      if (!ok_b && !done) {
+        if (!(mu > ipm_brk)) done = true;
+        else st = MPCB_STATUS_QP_FAIL;
+      }
+      __syncthreads();
+      QSTAMP(1);
+      {
+        Ctx<T> ra = r;
+        ra.w.DDX = r.wm.DAX;
+        ra.w.DDU = r.wm.DAU;
+        forward<T, true, true, false>(ra, T(0), T(0), false);
+      }
+      __syncthreads();
+      QSTAMP(2);
+      // the affine step to the boundary alpha_a, mu_a = (S0 + alpha_a S1 + alpha_a^2 S2) / (2 rows),
+      // and per input row w = 1/s_l - 1/s_u, c = Delta s_a Delta lambda_a / s_l - (upper) into DC
+      // (the state entries zero: no state rows here)
+      T aa = T(1), S0 = T(0), S1 = T(0), S2 = T(0);
+      if (in) {
+#pragma unroll 4
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+          const T* ip = r.w.IP + (int64_t)k * 18;
+          const T d = r.wm.DAU[(int64_t)k * NU17 + m];
+          const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m], ll = ip[6 + m], lu = ip[12 + m];
+          const T dsl = d, dsu = -d;
+          const T dll = (-ll * sl - ll * dsl) / sl, dlu = (-lu * su - lu * dsu) / su;
+          if (dsl < T(0)) aa = fmin(aa, -sl / dsl);
+          if (dsu < T(0)) aa = fmin(aa, -su / dsu);
+          if (dll < T(0)) aa = fmin(aa, -ll / dll);
+          if (dlu < T(0)) aa = fmin(aa, -lu / dlu);
+          S0 += sl * ll + su * lu;
+          S1 += sl * dll + ll * dsl + su * dlu + lu * dsu;
+          S2 += dsl * dll + dsu * dlu;
+          T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N + NX17 + m;
+          dc[0] = T(1) / sl - T(1) / su;
+          dc[24] = dsl * dll / sl - dsu * dlu / su;
+        }
+      }
+      for (int k = 0; k < N; ++k) {
+        T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
+        dc[s] = T(0);
+        dc[24 + s] = T(0);
+      }
+      for (int k = t; k < N; k += LN) {
+        T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
+        dc[OM] = T(0);
+        dc[24 + OM] = T(0);
+      }
+      aa = row_min(aa);
+      const T mu_a = (row_sum(S0) + aa * row_sum(S1) + aa * aa * row_sum(S2)) / (T(2) * rows);
+      const T ratio = mu_a / mu;
+      const T sig3 = ratio * ratio * ratio;
+      const T sig = (sig3 != sig3) ? T(1) : fmin(fmax(sig3, T(0)), T(1));
+      smu = sig * mu;
+      __syncthreads();
+      QSTAMP(7);
+      // corrector: the vector Riccati pass for the corrector's gradient (new k), then its direction
+      backward_corr<T>(r, smu);
+      __syncthreads();
+      QSTAMP(8);
+      forward<T, true, true, false>(r, T(0), T(0), false);   // -> DDX, DDU
+      __syncthreads();
+      QSTAMP(9);
+      }
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       T amax = T(1) / T(IPM17_TAU);
       bool dfin = true;   // a finite direction from strictly positive slacks
       if (in) {
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           const T* ip = r.w.IP + (int64_t)k * 18;
           const T d = r.w.DDU[(int64_t)k * NU17 + m];
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
           const T ll = ip[6 + m], lu = ip[12 + m];
-          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          T tl = smu, tu = smu;
+          if constexpr (MEH) {
+            const T da = r.wm.DAU[(int64_t)k * NU17 + m];
+            targets(smu, sl, su, ll, lu, da, -da, tl, tu);
+          }
+          const T dll = (tl - ll * sl - ll * d) / sl, dlu = (tu - lu * su + lu * d) / su;
           dfin = dfin && sl > T(0) && su > T(0) && (d - d) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
           if (d < T(0)) amax = fmin(amax, -sl / d);
           if (d > T(0)) amax = fmin(amax, su / d);
@@ -832,7 +1049,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
           if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
         };
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 1; k < N; ++k) step_row(k, s);
         for (int k = 1 + t; k < N; k += LN) step_row(k, OM);
       }
@@ -856,14 +1073,19 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       part_n = T(0);
       res_n = T(0);
       if (!done && valid && in) {
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
           T* ip = r.w.IP + (int64_t)k * 18;
           const T d = r.w.DDU[(int64_t)k * NU17 + m];
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
           const T ll = ip[6 + m], lu = ip[12 + m];
-          const T dll = (smu - ll * sl - ll * d) / sl, dlu = (smu - lu * su + lu * d) / su;
+          T tl = smu, tu = smu;
+          if constexpr (MEH) {
+            const T da = r.wm.DAU[(int64_t)k * NU17 + m];
+            targets(smu, sl, su, ll, lu, da, -da, tl, tu);
+          }
+          const T dll = (tl - ll * sl - ll * d) / sl, dlu = (tu - lu * su + lu * d) / su;
           const T dun = ip[m] + alpha * d, lln = ll + alpha * dll, lun = lu + alpha * dlu;
           ip[m] = dun;
           ip[6 + m] = lln;
@@ -894,7 +1116,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           part_n += nr.ll * nr.sl + nr.lu * nr.su;
           res_n = fmax(res_n, fmax(fabs(nr.rl), fabs(nr.ru)));
         };
-#pragma unroll MPCB_Q17_ROWS_UNROLL
+#pragma unroll 4
         for (int k = 1; k < N; ++k) upd_row(k, s);
         for (int k = 1 + t; k < N; k += LN) upd_row(k, OM);
       }
@@ -936,10 +1158,12 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
 
 template <class T> hipError_t launch_riccati17q(const FullArgs<T>& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.nb + q17::GR - 1) / q17::GR));
-  if (a.box)
-    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true>), grid, dim3(64), 0, st, a);
+  if (a.box && !a.sbox && sizeof(T) == 8)
+    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true, true>), grid, dim3(64), 0, st, a);
+  else if (a.box)
+    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true, false>), grid, dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL((q17::riccati17q_kernel<T, false>), grid, dim3(64), 0, st, a);
+    hipLaunchKernelGGL((q17::riccati17q_kernel<T, false, false>), grid, dim3(64), 0, st, a);
   return hipGetLastError();
 }
 template hipError_t launch_riccati17q<double>(const FullArgs<double>&, hipStream_t);
