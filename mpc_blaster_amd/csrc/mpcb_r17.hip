@@ -687,7 +687,10 @@ __device__ __forceinline__ void targets(T smu, T sl, T su, T ll, T lu, T dsl_a, 
 // !OUT: the iterate into DX.  OUT: X = xbar + dx, U = ubar + du, u0 (when write).  Returns this
 // lane's finiteness.
 template <class T, bool GAIN, bool STEP, bool OUT>
-__device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool write) {
+__device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool write, T* ddx = nullptr, T* ddu = nullptr) {
+  // (STEP: the direction's arrays, DDX / DDU unless given: the predictor's DAX / DAU)
+  if (!ddx) ddx = r.w.DDX;
+  if (!ddu) ddu = r.w.DDU;
   const FullArgs<T>& a = r.a;
   const int t = r.t, s = r.s, N = a.N;
   const bool in = r.in;
@@ -743,9 +746,9 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     // the ring's loads dynamic and every wait a vmcnt(0)): each lane stores its own state, and the
     // input lanes' du or (every other lane, the same value) the state-8 entry
     if constexpr (STEP || !OUT) {
-      T* base = STEP ? r.w.DDX : r.w.DX;
+      T* base = STEP ? ddx : r.w.DX;
       base[(int64_t)k * NX17 + s] = dxs;
-      T* p2 = (STEP && in) ? r.w.DDU + (int64_t)k * NU17 + r.m : base + (int64_t)k * NX17 + OM;
+      T* p2 = (STEP && in) ? ddu + (int64_t)k * NU17 + r.m : base + (int64_t)k * NX17 + OM;
       *p2 = (STEP && in) ? du : dx8;
     }
     if constexpr (OUT) {
@@ -788,7 +791,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   });
   QSTAMP_DONE("fwd");
   if constexpr (STEP || !OUT) {
-    T* base = STEP ? r.w.DDX : r.w.DX;
+    T* base = STEP ? ddx : r.w.DX;
     base[(int64_t)N * NX17 + s] = dxs;
     base[(int64_t)N * NX17 + OM] = dx8;
   }
@@ -953,12 +956,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       }
       __syncthreads();
       QSTAMP(1);
-      {
-        Ctx<T> ra = r;
-        ra.w.DDX = r.wm.DAX;
-        ra.w.DDU = r.wm.DAU;
-        forward<T, true, true, false>(ra, T(0), T(0), false);
-      }
+      forward<T, true, true, false>(r, T(0), T(0), false, r.wm.DAX, r.wm.DAU);
       __syncthreads();
       QSTAMP(2);
       // the affine step to the boundary alpha_a, mu_a = (S0 + alpha_a S1 + alpha_a^2 S2) / (2 rows),
