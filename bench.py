@@ -92,29 +92,68 @@ def cpu_baseline(w, budget_s=12.0):
                 sample=f'{done} instances of {w["name"]} (N={w["N"]}, fp64, {kind}) in {t_used:.1f} s')
 
 
-def run(w, world, rank, dev, steps, warmup):
+class _DeviceClock:
+    """Device time of the timed region: HIP events on the launch stream (GPU ranks) or the host
+    clock (the CPU solver stub of the launcher test, tests/bench_stub.py)."""
+
+    def __init__(self, cuda: bool):
+        import torch
+        self.cuda = cuda
+        self.t = [0.0, 0.0]
+        if cuda:
+            self.stream = torch.cuda.current_stream()
+            self.ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
+    def sync(self):
+        if self.cuda:
+            import torch
+            torch.cuda.synchronize()
+
+    def mark(self, i):
+        if self.cuda:
+            self.ev[i].record(self.stream)
+        else:
+            self.t[i] = time.perf_counter()
+
+    def elapsed_ms(self):
+        return self.ev[0].elapsed_time(self.ev[1]) if self.cuda else (self.t[1] - self.t[0]) * 1e3
+
+
+def make_solver(w, B, dev, stub=None):
+    """The batched solver of one rank: the HIP library (BatchedMPC) or, for the launcher test
+    only, a CPU stand-in module with the same methods (``--solver-stub``)."""
+    box = w['box']
+    if stub:
+        import importlib
+        return importlib.import_module(stub).make_solver(w, B)
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    cfg = MPCConfig(N=w['N'], dtype=w['dtype'], lbu=np.zeros(4) if box else None,
+                    ubu=np.full(4, 65.0) if box else None, max_as_iter=w.get('max_as_iter', 200))
+    return BatchedMPC(cfg, max_batch=B, device=dev)
+
+
+def run(w, world, rank, dev, steps, warmup, stub=None, dump_gather=None):
     import torch
     import torch.distributed as dist
 
-    from mpc_blaster_amd import BatchedMPC, MPCConfig
     from mpc_blaster_amd.dist import StepPipeline
     B, N = w['batch'], w['N']
-    cfg = MPCConfig(N=N, dtype=w['dtype'], lbu=np.zeros(4) if w['box'] else None,
-                    ubu=np.full(4, 65.0) if w['box'] else None, max_as_iter=w.get('max_as_iter', 200))
-    mpc = BatchedMPC(cfg, max_batch=B, device=dev)
+    cuda = stub is None
+    mpc = make_solver(w, B, dev, stub)
+    clock = _DeviceClock(cuda)
     inp = mpc.gen_inputs(B, seed=w['seed'], id_offset=rank * B, ref=w['ref'], wind=w['wind'])
-    torch.cuda.synchronize()
-    tdt = cfg.torch_dtype
+    clock.sync()
+    tdt = mpc.dtype
+    odev = dev if cuda else 'cpu'
     traj = not w['hist']
 
     def make_outs():
-        return (torch.empty((B, 4), dtype=tdt, device=dev),
-                torch.empty((B, N + 1, 12), dtype=tdt, device=dev) if traj else None,
-                torch.empty((B, N, 4), dtype=tdt, device=dev) if traj else None,
-                torch.zeros((B,), dtype=torch.int32, device=dev))
+        return (torch.empty((B, 4), dtype=tdt, device=odev),
+                torch.empty((B, N + 1, 12), dtype=tdt, device=odev) if traj else None,
+                torch.empty((B, N, 4), dtype=tdt, device=odev) if traj else None,
+                torch.zeros((B,), dtype=torch.int32, device=odev))
     pipe = StepPipeline(make_outs, 'histogram' if w['hist'] else 'gather', world,
                         histogram=lambda u0, counts: mpc.histogram(u0, 0.0, 65.0, 64, counts=counts))
-    stream = torch.cuda.current_stream()
 
     def solve(o):
         mpc.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'], want_traj=traj, out=o)
@@ -127,25 +166,26 @@ def run(w, world, rank, dev, steps, warmup):
     for _ in range(warmup):
         step()
     drain()
-    torch.cuda.synchronize()
+    clock.sync()
     # one event pair around the K solves on the launch stream (an event record between the
     # steps costs ~18 us of device time per step at c2: tools/host_overhead.py)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    clock.sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
+    clock.mark(0)
     for i in range(steps):
         step()
-    ev1.record(stream)
+    clock.mark(1)
     drain()
-    torch.cuda.synchronize()
+    clock.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / steps   # device time per solve (collectives excluded at N=1)
+    kern_ms = clock.elapsed_ms() / steps   # device time per solve (collectives excluded at N=1)
     bad = pipe.bad_status()
+    if dump_gather and rank == 0:   # the gathered u0 [world*B, 4] (or histogram) of the last step
+        np.save(dump_gather, pipe.result().cpu().numpy())
     # per-phase device time (HIP events the library records on the launch stream around each
     # kernel); a separate pass so that reading the events does not serialise the timed region
     mpc.set_timing(True)
@@ -157,13 +197,13 @@ def run(w, world, rank, dev, steps, warmup):
     mpc.set_timing(False)
     phase_ms = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=odev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-        bb = torch.tensor([bad], dtype=torch.int64, device=dev)
+        bb = torch.tensor([bad], dtype=torch.int64, device=odev)
         dist.all_reduce(bb)
         bad = int(bb.item())
-        ph = torch.tensor([phase_ms[k] for k in sorted(phase_ms)], dtype=torch.float64, device=dev)
+        ph = torch.tensor([phase_ms[k] for k in sorted(phase_ms)], dtype=torch.float64, device=odev)
         dist.all_reduce(ph, op=dist.ReduceOp.MAX)
         phase_ms = dict(zip(sorted(phase_ms), ph.tolist()))
     qp = None
@@ -172,7 +212,7 @@ def run(w, world, rank, dev, steps, warmup):
         qp = dict(fwd_passes=float(st[:, 0].sum()), bwd_stages=float(st[:, 1].sum()),
                   mean_iters=float(st[:, 0].mean()), max_iters=int(st[:, 0].max()))
         if world > 1:
-            t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=dev)
+            t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=odev)
             dist.all_reduce(t)
             qp['fwd_passes'], qp['bwd_stages'] = float(t[0]) / world, float(t[1]) / world
     path = 'split (3 kernels)' if mpc.path == 'split' else 'fused (1 kernel)'
@@ -217,6 +257,13 @@ def kernel_flops(w, r, phase):
     return 480 * N * B
 
 
+def dispatches_per_phase(B: int) -> int:
+    """Launches of each split-path phase per solve of B instances (mpcb_capi.hip: chunks of
+    65536, or MPCB_CHUNK)."""
+    chunk = max(64, int(os.environ.get('MPCB_CHUNK') or 65536))
+    return -(-int(B) // chunk)
+
+
 def pmc_kernel(workload: str, kernel: str):
     """Counter-derived figures of one kernel from the committed PMC summary (tools/pmc_summary.py)."""
     p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
@@ -248,11 +295,18 @@ def summarize(w, r, world, steps):
     solve_tf = solve_flop / (r['kern_ms'] * 1e-3) / 1e12
     hbm_gbs = compulsory_bytes(w) * B / (r['kern_ms'] * 1e-3) / 1e9
     pk = pmc_kernel(w['name'], names[dom]) or {}
+    # the library launches each phase once per chunk of instances (mpcb_capi.hip mpcb_create:
+    # 65536, MPCB_CHUNK); the PMC summary is per dispatch, the phase time and the flop count per
+    # phase, so the counter figures are scaled to the phase (c5: 131072 = 2 dispatches)
+    disp = dispatches_per_phase(B)
     ex = pk.get('executed_flops_per_launch')
+    ex = ex * disp if ex else None
+    tr = pk.get('hbm_bytes_per_launch')
+    tr = tr * disp if tr else None
     roof = {'bound': 'valu', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': achieved_tf / peak, 'traffic': pk.get('hbm_bytes_per_launch'),
-            'kernel': names[dom], 'kernel_ms': ph[dom],
-            'flop_per_launch': flop,
+            'frac': achieved_tf / peak, 'traffic': tr,
+            'kernel': names[dom], 'kernel_ms': ph[dom], 'dispatches_per_phase': disp,
+            'flop_per_phase': flop, 'executed_flop_per_phase': ex,
             'executed_frac': (ex / (ph[dom] * 1e-3) / 1e12 / peak) if ex else None,
             'phase_ms': ph, 'phase_kernels': names,
             'phase_frac': {k: kernel_flops(w, r, k) / (ph[k] * 1e-3) / 1e12 / peak
@@ -270,12 +324,30 @@ def summarize(w, r, world, steps):
                      'phase_kernels docstring) / that time. executed_frac = counter-executed flops '
                      '(64 x SQ_INSTS_VALU_FLOPS_FP32/FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F32, '
                      'profiles/pmc_<workload>.json) over the same time. traffic = HBM bytes per '
-                     'launch of that kernel, (2 x FETCH_SIZE + WRITE_SIZE) from the same PMC run '
+                     'phase of that kernel (per-dispatch PMC x dispatches_per_phase), '
+                     '(2 x FETCH_SIZE + WRITE_SIZE) from the same PMC run '
                      '(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md). solve_* = every kernel '
                      'of the solve over the whole solve time.')}
     if r.get('qp'):
         roof['active_set'] = r['qp']
     return value, roof
+
+
+def launch_ranks(nproc: int, argv: list[str]) -> int:
+    """``bench.py --gpus N`` without an outer launcher: start N ranks of this same script under
+    ``torch.distributed.run`` (one process per GPU, rendezvous on 127.0.0.1) as CHILD processes
+    and return their worst exit code.  The parent imports nothing that touches the GPU (no torch
+    at all) and never execs: every HIP context lives in a child."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={nproc}',
+           '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0', OMP_NUM_THREADS=os.environ.get('OMP_NUM_THREADS', '1'))
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -290,7 +362,15 @@ def main():
     ap.add_argument('--no-latency', action='store_true', help='skip the B=1 per-step latency block')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     ap.add_argument('--max-as-iter', type=int, default=200, help='active-set cap (box workload)')
+    # launcher test only (tests/test_bench_launch.py): gloo ranks on the CPU with a stand-in solver
+    ap.add_argument('--backend', default='nccl', choices=('nccl', 'gloo'), help=argparse.SUPPRESS)
+    ap.add_argument('--solver-stub', default=None, help=argparse.SUPPRESS)
+    ap.add_argument('--dump-gather', default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # no outer launcher: spawn the N ranks ourselves, before anything initialises a GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -302,16 +382,26 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
+    if 'WORLD_SIZE' in os.environ and args.gpus != world:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
+    cuda = args.solver_stub is None
+    if cuda and args.backend != 'nccl':
+        raise SystemExit('--backend gloo is for the CPU solver stub only')
+    if cuda:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+        dev = torch.cuda.current_device()
     else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
+        dev = 'cpu'
+    if world > 1:
+        if cuda:
+            dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+        else:
+            dist.init_process_group('gloo')
 
-    r = run(w, world, rank, dev, args.steps, args.warmup)
+    r = run(w, world, rank, dev, args.steps, args.warmup, stub=args.solver_stub,
+            dump_gather=args.dump_gather)
     sec = None
-    if world == 1 and not args.no_secondary and args.workload == 'c2':
+    if world == 1 and cuda and not args.no_secondary and args.workload == 'c2':
         w3 = dict(WORKLOADS['c3'], name='c3')
         r3 = run(w3, 1, 0, dev, args.steps, args.warmup)
         v3, roof3 = summarize(w3, r3, 1, args.steps)
@@ -346,9 +436,11 @@ def main():
             'roofline': roof,
             'bad_status': r['bad'],
         }
+        if not cuda:
+            line['data'] += f'; CPU solver stub {args.solver_stub} over {args.backend} (launcher test)'
         if sec is not None:
             line['secondary'] = sec
-        if world == 1 and args.workload == 'c2' and not args.no_latency:
+        if world == 1 and cuda and args.workload == 'c2' and not args.no_latency:
             from mpc_blaster_amd.latency import measure_b1
             line['latency_b1'] = measure_b1(device=dev)
         if not args.no_cpu_baseline and world == 1:

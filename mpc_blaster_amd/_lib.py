@@ -89,6 +89,12 @@ def load(path: str | None = None):
     for name in EXPORTS:
         if name not in ('mpcb_last_error', 'mpcb_workspace_bytes'):
             getattr(lib, name).restype = i32
+    got = int(lib.mpcb_abi_version())
+    if got != ABI_VERSION:
+        # a stale library would read arguments of a changed signature as the wrong types
+        # (mpcb_set_params gained two arguments in v4), so refuse it before any call
+        raise LibraryMissing(f'{p} has C ABI version {got}, this binding expects {ABI_VERSION}: '
+                             'rebuild it (__graft_entry__.build())')
     if path is None:
         _lib = lib
     return lib

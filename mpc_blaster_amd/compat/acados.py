@@ -125,14 +125,15 @@ class AcadosOcpSolver:
 
     def _upload_params(self):
         """Hand the per-stage parameters to the device (acados keeps p per stage; the terminal
-        stage has no dynamics, so stages 0..N-1 are what the solve reads)."""
-        self._p_dirty = False
+        stage has no dynamics, so stages 0..N-1 are what the solve reads).  The dirty flag is
+        cleared only once the device has accepted them: a rejected set keeps failing."""
         p = self._p[:, :self.N]
         if self.nx == NX_REF:
             same_stages = bool(np.all(p == p[:, :1]))
             same_rows = bool(np.all(p == p[:1]))
             self.mpc.set_params(p[:1, 0] if (same_stages and same_rows) else
                                 (p[:, 0] if same_stages else p))
+            self._p_dirty = False
             return
         # 12/4 slice: T_blast (p[24]) is the model's only parameter there, a handle scalar
         t = p[..., 24]
@@ -144,6 +145,7 @@ class AcadosOcpSolver:
                           'model does not carry; ignored', stacklevel=3)
         if float(t.flat[0]) != self.cfg.t_blast:
             self.mpc.set_t_blast(float(t.flat[0]))
+        self._p_dirty = False
 
     def cost_set(self, stage: int, field: str, value):
         if field != 'yref':

@@ -1,0 +1,56 @@
+"""bench.py's own multi-rank launcher (``--gpus N`` without torchrun): the parent starts N ranks
+under torch.distributed.run before anything touches a GPU, rank 0 prints ONE JSON line with
+n_gpus = N and global_batch = N*B, and the gathered u0 equals an unsharded solve.  Run here over
+gloo with the CPU solver stub (tests/bench_stub.py) standing in for the HIP handle."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(tmp_path, workload, gpus, batch, steps=2):
+    dump = str(tmp_path / f'gather_{workload}.npy')
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get('PYTHONPATH', ''),
+               OMP_NUM_THREADS='1')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', str(gpus),
+                        '--steps', str(steps), '--warmup', '1', '--workload', workload,
+                        '--batch', str(batch), '--no-cpu-baseline', '--backend', 'gloo',
+                        '--solver-stub', 'tests.bench_stub', '--dump-gather', dump],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0]), np.load(dump)
+
+
+@pytest.mark.parametrize('workload,gpus,batch', [('c2', 2, 12), ('c5', 2, 10)])
+def test_bench_gpus_n_launches_n_ranks(tmp_path, workload, gpus, batch):
+    from oracle.inputs import make_inputs
+    from oracle.ocp import OcpSpec, mpc_solve
+    line, got = _run_bench(tmp_path, workload, gpus, batch)
+    assert line['n_gpus'] == gpus
+    assert line['config']['global_batch'] == gpus * batch
+    assert line['value'] > 0 and line['bad_status'] == 0
+    N = 20 if workload == 'c2' else 40
+    inp = make_inputs(workload, ids=np.arange(gpus * batch, dtype=np.uint64), N=N)
+    ref = mpc_solve(inp['x0'], inp['xref'], inp['uref'], OcpSpec(N=N), wind=inp['wind'])['u0']
+    if workload == 'c2':   # the RCCL/gloo all-gather of u0 in global id order
+        assert got.shape == (gpus * batch, 4)
+        assert np.array_equal(got, ref)
+    else:                  # the all-reduced per-motor histogram
+        b = np.clip(np.floor(ref * (64 / 65.0)), 0, 63).astype(np.int64)
+        want = np.stack([np.bincount(b[:, m], minlength=64) for m in range(4)])
+        assert np.array_equal(got, want)
+
+
+def test_bench_gpus_1_runs_in_process(tmp_path):
+    line, got = _run_bench(tmp_path, 'c2', 1, 8, steps=1)
+    assert line['n_gpus'] == 1 and line['config']['global_batch'] == 8
+    assert got.shape == (8, 4)

@@ -95,3 +95,21 @@ def test_set_p_on_the_slice_maps_t_blast_and_rejects_stage_varying():
     o.set(1, 'p', p)
     with pytest.raises(NotImplementedError):
         o._upload_params()
+    assert o._p_dirty    # the rejected parameters stay pending: the next solve() raises again
+    with pytest.raises(NotImplementedError):
+        o._upload_params()
+
+
+def test_library_abi_version_is_checked_at_load(tmp_path):
+    """A library of another C ABI version is refused before any call (a stale v3
+    library would read mpcb_set_params' row count as its device pointer)."""
+    import subprocess
+
+    from mpc_blaster_amd import _lib
+    src = tmp_path / 'stale.c'
+    src.write_text('int mpcb_abi_version(void) { return 3; }\n' + ''.join(
+        f'int {n}(void) {{ return 0; }}\n' for n in _lib.EXPORTS if n != 'mpcb_abi_version'))
+    so = tmp_path / 'libstale.so'
+    subprocess.check_call(['gcc', '-shared', '-fPIC', str(src), '-o', str(so)])
+    with pytest.raises(_lib.LibraryMissing, match='ABI version 3'):
+        _lib.load(str(so))
