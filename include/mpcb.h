@@ -40,7 +40,12 @@ enum {
   MPCB_E_NOMEM = -3,     /* workspace allocation failed */
   MPCB_E_UNSUPPORTED = -4
 };
-enum { MPCB_STATUS_OK = 0, MPCB_STATUS_NAN = 1, MPCB_STATUS_MAXITER = 2, MPCB_STATUS_QP_FAIL = 4 };
+/* per-instance solver status, acados' codes (ACADOS_SUCCESS, _NAN_DETECTED, _MAXITER, _MINSTEP,
+ * _QP_FAILURE).  MINSTEP: the fp64 17/6 interior point stopped at its conditioning limit (a
+ * breakdown or collapsed step once mu <= 1e-5 on a feasible iterate) and the active-set polish did
+ * not certify the point: the outputs are that reduced-accuracy iterate. */
+enum { MPCB_STATUS_OK = 0, MPCB_STATUS_NAN = 1, MPCB_STATUS_MAXITER = 2, MPCB_STATUS_MINSTEP = 3,
+       MPCB_STATUS_QP_FAIL = 4 };
 
 #define MPCB_MAX_NX 17
 #define MPCB_MAX_NU 6
@@ -198,12 +203,14 @@ int mpcb_poc_jacobians(int64_t B, const double* pose, double stream_velocity, co
                        double* J_pos, double* p25, int32_t* status, void* hip_stream);
 
 /*
- * Work statistics of the last solve on a 12/4 input-box handle (the active-set QP, c4): per
+ * Work statistics of the last solve on an input-box handle.  12/4 (the active-set QP, c4): per
  * instance ``out[2b]`` = forward passes until its active set was the KKT point (including the
  * first, after the unconstrained Riccati pass) and ``out[2b+1]`` = backward stages its masked
- * Riccati passes recomputed (restarts skip the stages above the highest changed one).  ``out``
- * is a DEVICE int32 array [B, 2], B <= that solve's batch.  No reference counterpart (HPIPM's
- * ``get_stats('qp_iter')``).  MPCB_E_UNSUPPORTED on other handles.
+ * Riccati passes recomputed (restarts skip the stages above the highest changed one).  17/6 (the
+ * interior point): ``out[2b]`` = interior-point iterations (Newton directions computed),
+ * ``out[2b+1]`` = polish passes (fp64 state box).  ``out`` is a DEVICE int32 array [B, 2], B <= that
+ * solve's batch.  Reference counterpart: HPIPM's ``get_stats('qp_iter')``.  MPCB_E_UNSUPPORTED on
+ * handles without an input box.
  */
 int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* hip_stream);
 

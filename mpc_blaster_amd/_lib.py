@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 ABI_VERSION = 4
 MPCB_F64, MPCB_F32 = 0, 1
 MPCB_MAX_NX, MPCB_MAX_NU = 17, 6
-STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
+STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_MINSTEP, STATUS_QP_FAIL = 0, 1, 2, 3, 4
 
 EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',

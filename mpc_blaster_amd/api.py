@@ -197,8 +197,9 @@ class BatchedMPC:
         self.cfg.t_blast = float(t_blast)
 
     def qp_stats(self, B=None):
-        """Input-box (12/4) work statistics of the last solve: int32 [B, 2] device tensor of
-        (forward passes, masked backward stages) per instance (mpcb_qp_stats)."""
+        """Input-box work statistics of the last solve: int32 [B, 2] device tensor per instance
+        (mpcb_qp_stats): 12/4 (forward passes, masked backward stages); 17/6 (interior-point
+        iterations, polish passes)."""
         torch = _torch()
         B = self._u0.shape[0] if B is None else int(B)
         out = torch.empty((B, 2), dtype=torch.int32, device=f'cuda:{self.device}')

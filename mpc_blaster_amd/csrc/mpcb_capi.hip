@@ -65,7 +65,6 @@ struct mpcb_handle {
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
   int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
-  int q17 = 1;            // 17/6: the 16-lane DPP Riccati / interior-point kernel (MPCB_R17=0: riccati17_kernel)
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
   Model<double> Md;
@@ -209,7 +208,6 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     if (chunk > max_batch) chunk = max_batch;
     h->full = 1;
     h->split = 1;
-    if (const char* e = getenv("MPCB_R17")) h->q17 = atoi(e) != 0;
     h->chunk = chunk;
     // (+3 instances: a ragged last wavefront of the 16-lane kernel works in private padding slots)
     h->chunk_elems = full17_elems(cfg->N) * ((chunk + 3) / 4 * 4);
@@ -291,7 +289,7 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     delete h;
     return fail(MPCB_E_HIP, "weights upload: %s", hipGetErrorString(e));
   }
-  if (!full && h->split && cfg->box_u) {
+  if (cfg->box_u && (full || h->split)) {
     e = hipMalloc((void**)&h->qp_stats, (size_t)max_batch * 2 * sizeof(int32_t));
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
@@ -319,7 +317,7 @@ extern "C" int mpcb_destroy(mpcb_handle* h) {
 
 extern "C" int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* stream) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
-  if (!h->qp_stats) return fail(MPCB_E_UNSUPPORTED, "QP statistics are kept by the 12/4 input-box path");
+  if (!h->qp_stats) return fail(MPCB_E_UNSUPPORTED, "QP statistics are kept by input-box handles");
   if (B < 0 || B > h->qp_stats_rows)
     return fail(MPCB_E_INVALID, "batch %lld exceeds the last boxed solve's %lld instances", (long long)B,
                 (long long)h->qp_stats_rows);
@@ -355,7 +353,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.box = h->cfg.box_u;
     a.sbox = h->cfg.box_x;
     a.max_as_iter = h->cfg.max_as_iter;
-    a.q17 = h->q17;
+    a.qp_stats = h->qp_stats;
     int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
       a.b0 = b0;
@@ -367,6 +365,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     }
     h->timed_chunks = h->timing ? (chunk_i < mpcb_handle::TCHUNKS ? chunk_i : mpcb_handle::TCHUNKS) : 0;
     h->timed_split = 1;
+    if (h->qp_stats) h->qp_stats_rows = B;
     return MPCB_OK;
   }
   if (h->split) {

@@ -224,7 +224,7 @@ struct FullArgs {
   int box;           // input box lbu <= u <= ubu (interior-point iterations)
   int sbox;          // with box: state box lbx <= x_k <= ubx on stages 1..N-1
   int max_as_iter;   // iteration cap
-  int q17;           // the 16-lane DPP Riccati / interior-point kernel (mpcb_r17.hip); 0: riccati17_kernel
+  int32_t* qp_stats; // boxes: per instance [interior-point iterations, polish passes] (mpcb_qp_stats)
 };
 
 __host__ __device__ constexpr int64_t full17_elems(int N) {
@@ -318,8 +318,13 @@ struct WsM17 {
 };
 
 constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.995, IPM17_THETA = 0.1;
-// (IPM17_BREAK: oracle.ocp.IPM_BREAK_TOL, where the choice of 1e-6 is explained)
+// (IPM17_BREAK: oracle.ocp.IPM_BREAK_TOL, where the choice of 1e-5 is explained: an fp64 exit
+// there that the polish below does not certify ends MPCB_STATUS_MINSTEP, not OK)
 constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-5, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
+// the fp64 state-box polish (oracle.ocp.al_polish): augmented-Lagrangian passes over the
+// interior point's active set with one active-set change per pass
+constexpr double POL17_RHO = 1e10, POL17_EQ = 1e-10, POL17_FEAS = 1e-10;
+constexpr int POL17_ITERS = 12;
 constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
 constexpr int IPM17_SHORT_RUN = 10;
 // fp32: the duality measure stops near 1e-6 (lambda / s reaches the fp32 conditioning limit

@@ -1,7 +1,6 @@
 // mpcb_r17.hip — the 17/6 Riccati pass and its interior point in a 16-lane DPP layout
 // (blastermodel.py:214-292, acados_ocp_blasterModel.json: N = 60, nx = 17,
-// nu = 6).  Same arithmetic as riccati17_kernel (mpcb_full.hip), which stays as the reference
-// implementation behind MPCB_R17=0; this kernel is the default.
+// nu = 6).
 //
 // Layout.  Four instances per wavefront, 16 lanes each (one DPP row per instance), so every
 // operand exchange inside an instance is a row broadcast folded into the consuming FMA
@@ -284,8 +283,12 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
 // terms and the iterate shift when r.a.box).  Writes K (row-major 6 x 17) and k to KR.  With the
 // box, the previous iteration's step of the state trajectory, dx += apend ddx, is applied here
 // stage by stage (written back to DX) instead of in a pass of its own.
-template <class T, bool MEH = false>
-__device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0)) {
+// POLC (the fp64 state-box kernel): with pol (this group polishes, oracle.ocp.al_polish) every
+// row takes the augmented-Lagrangian terms of its active side instead of the barrier: D = rho and
+// d = nu + rho (y - b) on an active row (side != 0), nothing on an inactive one.  The rows then hold
+// (nu, side) where the multipliers (lambda_l, lambda_u) were: IP[6 + m], IP[12 + m] and IX rows 2, 3.
+template <class T, bool MEH = false, bool POLC = false>
+__device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0), bool pol = false) {
   const FullArgs<T>& a = r.a;
   const bool ipm = a.box != 0;
   const bool gaps = !ipm && a.mode == MPCB_MODE_ITERATE;
@@ -409,8 +412,15 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
       }
       if (ipm) {
         const T sl = ic.du - (lbm - cu.ub), su = (ubm - cu.ub) - ic.du;
-        L.HU[m][m] += ic.ll / sl + ic.lu / su;
-        hu -= smu * (T(1) / sl - T(1) / su);
+        T D = ic.ll / sl + ic.lu / su, d = -smu * (T(1) / sl - T(1) / su);
+        if constexpr (POLC) {
+          const bool act = ic.lu != T(0);
+          const T bnd = ic.lu < T(0) ? lbm - cu.ub : ubm - cu.ub;
+          D = pol ? (act ? T(POL17_RHO) : T(0)) : D;
+          d = pol ? (act ? ic.ll + T(POL17_RHO) * (ic.du - bnd) : T(0)) : d;
+        }
+        L.HU[m][m] += D;
+        hu += d;
       }
       L.HU[m][6] = hu;
       L.HU[m][7] = g8;
@@ -474,11 +484,20 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0))
     }
     if (sbox && k > 0) {   // state-box rows of this stage: barrier terms on the state diagonals
       T D, d;
-      SRow<T>(ic.dxs, cu.xs, lbs, ubs, ic.ixs[0], ic.ixs[1], ic.ixs[2], ic.ixs[3]).barrier(smu, D, d);
+      auto rowterms = [&](T y, T xb, T lb, T ub, const T (&ix)[4]) {
+        SRow<T>(y, xb, lb, ub, ix[0], ix[1], ix[2], ix[3]).barrier(smu, D, d);
+        if constexpr (POLC) {   // (nu, side) in rows 2, 3; bounds in dx coordinates
+          const bool act = ix[3] != T(0);
+          const T bnd = (ix[3] < T(0) ? lb : ub) - xb;
+          D = pol ? (act ? T(POL17_RHO) : T(0)) : D;
+          d = pol ? (act ? ix[2] + T(POL17_RHO) * (y - bnd) : T(0)) : d;
+        }
+      };
+      rowterms(ic.dxs, cu.xs, lbs, ubs, ic.ixs);
 #pragma unroll
       for (int i = 0; i < NX17; ++i) Gs[i] += (i == s) ? D : T(0);
       hs += d;
-      SRow<T>(ic.dx8, cu.x8, lb8, ub8, ic.ix8[0], ic.ix8[1], ic.ix8[2], ic.ix8[3]).barrier(smu, D, d);
+      rowterms(ic.dx8, cu.x8, lb8, ub8, ic.ix8);
       G88 += D;
       h8 += d;
     }
@@ -806,8 +825,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   return fin;
 }
 
-// The interior point of mpcb_full.hip riccati17_kernel<T, true> (same iteration as
-// oracle.ocp.ipm_box_solve) in this layout: input rows owned by the input lanes, state rows by the
+// The interior point (the iteration of oracle.ocp.ipm_box_solve) in this layout: input rows owned by the input lanes, state rows by the
 // owner of the state, the rows of state 8 spread over the lanes by stage (k = 1 + t, 1 + t + 16 ..).
 // MEH (fp64, the input box alone): Mehrotra's predictor-corrector (oracle.ocp._ipm_box_mehrotra)
 // instead of the adaptive centring.
@@ -880,6 +898,36 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     }
     __syncthreads();
     const T rows = T(N * NU17 + (sbox ? (N - 1) * NX17 : 0));
+    // the fp64 state-box polish (oracle.ocp.al_polish, mpcb_full.h POL17_*): once a group's interior
+    // point has converged (pst 0 -> 1) its rows are classified and it runs up to POL17_ITERS
+    // augmented-Lagrangian passes through the same backward / forward call sites as the interior
+    // point, while the other groups of the wave may still iterate; 2 = polished (the group keeps
+    // re-solving its frozen last pass, which reproduces its direction bit for bit), 3 = finished
+    // without a polished point (failure, the iteration cap, or a polish that did not certify)
+    constexpr bool POLC = sizeof(T) == 8 && !MEH;
+    const bool polish = POLC && sbox;
+    int pst = 0, npass = 0, nit = 0;   // (nit: this group's interior-point iterations)
+    bool early = false;    // stopped at the conditioning limit (breakdown / collapsed step)
+    const int it_max = a.max_as_iter + (polish ? POL17_ITERS : 0);
+    auto classify = [&]() {   // side = -1 (lower) / +1 (upper) / 0, nu = lambda_u - lambda_l
+      auto cl = [&](T sl, T su, T ll, T lu, T& nu, T& side) {
+        side = ll > sl ? T(-1) : (lu > su ? T(1) : T(0));
+        nu = side != T(0) ? lu - ll : T(0);
+      };
+      if (in) {
+        for (int k = 0; k < N; ++k) {
+          const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+          T* ip = r.w.IP + (int64_t)k * 18;
+          cl(ip[m] - (lbm - ubk), (ubm - ubk) - ip[m], ip[6 + m], ip[12 + m], ip[6 + m], ip[12 + m]);
+        }
+      }
+      auto clrow = [&](int k, int i) {
+        T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
+        cl(ix[0], ix[NX17], ix[2 * NX17], ix[3 * NX17], ix[2 * NX17], ix[3 * NX17]);
+      };
+      for (int k = 1; k < N; ++k) clrow(k, s);
+      for (int k = 1 + t; k < N; k += LN) clrow(k, OM);
+    };
     bool done = false;
     T prev_alpha = T(1);
     int nshort = 0;
@@ -890,7 +938,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
     const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
     QSTAMP_INIT();
-    for (int it = 0; it < a.max_as_iter; ++it) {
+    for (int it = 0; it < it_max; ++it) {
       QSTAMP(6);
       // duality measure mu = mean(lambda s), primal residual of the state rows: a pass over the
       // rows at the start, afterwards summed by the update pass of the previous iteration (same
@@ -926,33 +974,122 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       if (sbox) res = row_max(res);
       }
       done = done || (!(mu > ipm_tol) && !(res > ipm_res));
-      if (__all(done || !valid)) break;
+      if (polish) {
+        if (it == a.max_as_iter && !done) {   // the interior point's own cap
+          done = true;
+          st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+        }
+        if (pst == 0 && done) {
+          if (st == MPCB_STATUS_OK && valid) {
+            classify();
+            pst = 1;
+          } else {
+            pst = 3;
+          }
+        }
+        __syncthreads();   // the rows of state 8 are read by every lane of the next backward
+      }
+      if (__all((polish ? pst >= 2 : done) || !valid)) break;
       QSTAMP(0);
       T smu;
       if constexpr (!MEH) {
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
+      nit += (pst == 0 && !done) ? 1 : 0;
       smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
-      const bool ok_b = backward<T>(r, smu, apend);
+      const bool ok_b = backward<T, false, POLC>(r, smu, apend, pst == 1 || pst == 2);
       apend = T(0);
       if (!ok_b && !done) {
         // a Newton system that lost positive definiteness near the solution: keep the current
         // iterate as converged; earlier it is a failure
-        if (!(mu > ipm_brk) && !(res > ipm_res)) done = true;
-        else st = MPCB_STATUS_QP_FAIL;
+        if (!(mu > ipm_brk) && !(res > ipm_res)) {
+          done = true;
+          early = true;
+        } else {
+          st = MPCB_STATUS_QP_FAIL;
+        }
       }
       __syncthreads();
       QSTAMP(1);
-      forward<T, true, true, false>(r, T(0), T(0), false);   // the Newton step -> DDX, DDU
+      const bool ffin = forward<T, true, true, false>(r, T(0), T(0), false);   // the Newton step -> DDX, DDU
       __syncthreads();
       QSTAMP(2);
+      if (polish && __any(pst == 1)) {
+        // one polish pass: rows at z0 + Delta, nu <- nu + rho (y - b) on the active rows, and one
+        // active-set change per group (the release of the most negative signed multiplier, else
+        // the fix of the inactive row furthest outside its bound)
+        const bool pfail = row_or((ok_b && ffin) ? 0 : 1) != 0;
+        const bool live = pst == 1 && !pfail;
+        T eq_l = T(0), w_l = T(INFINITY), v_l = T(-INFINITY), vside = T(0);
+        int wk = 0, wkind = 0, vk = 0, vkind = 0;
+        auto prow = [&](int k, int kind, T y, T lb, T ub, T* nup, T side) {
+          if (side != T(0)) {
+            const T e = y - (side < T(0) ? lb : ub);
+            eq_l = fmax(eq_l, fabs(e));
+            const T nun = *nup + T(POL17_RHO) * e;
+            if (side * nun < w_l) {
+              w_l = side * nun;
+              wk = k;
+              wkind = kind;
+            }
+            if (live) *nup = nun;
+          } else {
+            const T v = fmax(lb - y, y - ub);
+            if (v > v_l) {
+              v_l = v;
+              vk = k;
+              vkind = kind;
+              vside = y < lb ? T(-1) : T(1);
+            }
+          }
+        };
+        if (in) {
+          for (int k = 0; k < N; ++k) {
+            const T ubk = r.w.UB[(int64_t)k * NU17 + m];
+            T* ip = r.w.IP + (int64_t)k * 18;
+            prow(k, 0, ip[m] + r.w.DDU[(int64_t)k * NU17 + m], lbm - ubk, ubm - ubk, ip + 6 + m, ip[12 + m]);
+          }
+        }
+        auto srow = [&](int k, int i, int kind) {
+          const int64_t kx = (int64_t)k * NX17 + i;
+          const T xb = r.w.XB[kx];
+          T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
+          prow(k, kind, r.w.DX[kx] + r.w.DDX[kx], W.lbx[i] - xb, W.ubx[i] - xb, ix + 2 * NX17, ix[3 * NX17]);
+        };
+        for (int k = 1; k < N; ++k) srow(k, s, 1);
+        for (int k = 1 + t; k < N; k += LN) srow(k, OM, 2);
+        const T eq = row_max(eq_l), wmin = row_min(w_l), vmax = row_max(v_l);
+        const bool rel = wmin < T(0);
+        const bool add = !rel && vmax > T(POL17_FEAS);
+        // the lowest lane holding the extreme row makes the change
+        const bool cand = rel ? (w_l == wmin) : (add && v_l == vmax);
+        const bool win = live && (rel || add) && row_min(cand ? T(t) : T(LN)) == T(t);
+        if (win) {
+          const int k = rel ? wk : vk, kind = rel ? wkind : vkind;
+          const T side = rel ? T(0) : vside;
+          T* slot = kind == 0 ? r.w.IP + (int64_t)k * 18 + 6 + m
+                              : r.w.IX + (int64_t)k * 4 * NX17 + 2 * NX17 + (kind == 1 ? s : OM);
+          slot[0] = T(0);                              // nu
+          slot[kind == 0 ? 6 : NX17] = side;           // side
+        }
+        if (pst == 1) {
+          ++npass;
+          pst = pfail ? 3 : (!rel && !add && !(eq > T(POL17_EQ))) ? 2 : (npass >= POL17_ITERS ? 3 : 1);
+        }
+        __syncthreads();
+      }
       } else {
       // predictor: targets 0 -> the affine direction into DAX / DAU (K, k, the factor of Huu and
       // the stage gradients stay in KR / LC / GV)
+      nit += !done ? 1 : 0;
       const bool ok_b = backward<T, true>(r, T(0), apend);
       apend = T(0);
       if (!ok_b && !done) {
-        if (!(mu > ipm_brk)) done = true;
-        else st = MPCB_STATUS_QP_FAIL;
+        if (!(mu > ipm_brk)) {
+          done = true;
+          early = true;
+        } else {
+          st = MPCB_STATUS_QP_FAIL;
+        }
       }
       __syncthreads();
       QSTAMP(1);
@@ -1059,6 +1196,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       prev_alpha = alpha;
       if (!done && dbad) {   // no usable direction: converged near the solution, else a failure
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
+        else early = true;
         done = true;
       }
       nshort = (alpha < T(IPM17_SHORT)) ? nshort + 1 : 0;
@@ -1066,6 +1204,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         // collapsed step, or a run of short ones: converged near the solution (conditioning
         // limit), else an infeasible QP
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;
+        else early = true;
         done = true;
       }
       part_n = T(0);
@@ -1125,13 +1264,24 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     QSTAMP(5);
     QSTAMP_DONE("ipm");
     if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
-    // outputs: X = xbar + dx, U = ubar + du of the final iterate
+    // an fp64 stop at the conditioning limit that no polish certified: reduced accuracy, acados'
+    // MINSTEP (the fp32 interior point stops there by design: its tolerances are scaled)
+    if (sizeof(T) == 8 && st == MPCB_STATUS_OK && early && pst != 2) st = MPCB_STATUS_MINSTEP;
+    if (valid && t == 0 && a.qp_stats) {
+      a.qp_stats[2 * b] = nit;
+      a.qp_stats[2 * b + 1] = npass;
+    }
+    // outputs: X = xbar + dx, U = ubar + du of the final iterate (+ the polish's Delta)
     fin = true;
     for (int k = 0; k <= N; ++k) {   // (with the last step, when it is still pending)
       T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
       if (apend != T(0)) {
         xs = xs + apend * r.w.DDX[(int64_t)k * NX17 + s];
         x8 = x8 + apend * r.w.DDX[(int64_t)k * NX17 + OM];
+      }
+      if (POLC && pst == 2) {
+        xs = xs + r.w.DDX[(int64_t)k * NX17 + s];
+        x8 = x8 + r.w.DDX[(int64_t)k * NX17 + OM];
       }
       if (valid && a.X) {
         T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
@@ -1140,7 +1290,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       }
       fin = fin && ((xs - xs) == T(0)) && ((x8 - x8) == T(0));
       if (in && k < N) {
-        const T uo = r.w.UB[(int64_t)k * NU17 + m] + r.w.IP[(int64_t)k * 18 + m];
+        T duk = r.w.IP[(int64_t)k * 18 + m];
+        if (POLC && pst == 2) duk = duk + r.w.DDU[(int64_t)k * NU17 + m];
+        const T uo = r.w.UB[(int64_t)k * NU17 + m] + duk;
         fin = fin && ((uo - uo) == T(0));
         if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + m] = uo;
         if (valid && k == 0) a.u0[b * NU17 + m] = uo;

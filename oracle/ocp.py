@@ -43,7 +43,7 @@ from .model import Params, f12
 from .rk4 import rk4_sens, rk4_step
 
 NX, NU = 12, 4
-STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_QP_FAIL = 0, 1, 2, 4
+STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_MINSTEP, STATUS_QP_FAIL = 0, 1, 2, 3, 4   # acados' codes
 
 
 def default_Q() -> np.ndarray:
@@ -446,6 +446,8 @@ def _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60
     mu, res = measure()
     status = np.where(conv | ((mu <= IPM_TOL) & (res <= 1e-9)), STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
+    # a stop at the conditioning limit (breakdown / collapsed step) is a reduced-accuracy iterate
+    status = np.where((status == STATUS_OK) & ~((mu <= IPM_TOL) & (res <= 1e-9)), STATUS_MINSTEP, status).astype(np.int32)
     return dx, du, status, it
 
 
@@ -597,7 +599,124 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
     mu, res = measure()
     status = np.where(conv | ((mu <= IPM_TOL) & (res <= 1e-9)), STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
+    acc = np.zeros(Bsz, dtype=bool)
+    if sx and POLISH_ITERS > 0:
+        rows_u = (du, lbu, ubu, sul, suu, llu, luu)
+        rows_x = (dx[:, 1:N], lbx_, ubx_, sxl, sxu, llx, lux)
+        pdx, pdu, acc = al_polish(A, Bm, xbar, ubar, xref, uref, spec, dx, du, rows_u, rows_x,
+                                  status == STATUS_OK)
+        dx = np.where(acc[:, None, None], pdx, dx)
+        du = np.where(acc[:, None, None], pdu, du)
+    # an early exit (breakdown or stall at the conditioning limit) that no polish certified keeps its
+    # reduced-accuracy iterate under acados' MINSTEP status, not OK
+    status = np.where((status == STATUS_OK) & ~acc & ~((mu <= IPM_TOL) & (res <= 1e-9)),
+                      STATUS_MINSTEP, status).astype(np.int32)
     return dx, du, status, it
+
+
+# The polish after the state-box interior point (HPIPM's analogue: its final "exact" step on the
+# identified active set).  At the interior point's last iterate a row is taken as active on its
+# lower side when lambda_l > s_l (upper likewise): on a strongly active row lambda / s ~ 1e4..1e16,
+# on an inactive one ~1e-2 or less.  The equality-constrained QP on that active set is solved by the
+# method of multipliers over the same Riccati recursion: each pass is one linear solve, the
+# minimiser of the augmented Lagrangian  J + nu'(Cz - b) + rho/2 |Cz - b|^2  (diagonal rho on the
+# active rows, gradient nu + rho (y - b): the interior point's D / d slots), linearised at the
+# interior point's iterate z0 (the QP is quadratic, so the minimiser does not depend on it), then
+# nu <- nu + rho (y - b).  nu starts at lambda_u - lambda_l.  Near the conditioning limit the ratio
+# test can take a row that is not active at the solution (the thin-interior fixture: 2 of 356 rows,
+# whose equalities are then inconsistent with the others and whose multipliers run off with the
+# wrong sign), so every pass also corrects the set as a primal-dual active-set step would: an
+# active row whose multiplier has the wrong sign is released (nu = 0), an inactive row outside its
+# bound is fixed at it (nu = 0).  An instance is done when its set did not change and every active
+# row is within POLISH_EQ of its bound; it then keeps the polished point if the Riccati recursion
+# stayed positive definite.  An instance not done after POLISH_ITERS passes keeps the interior-point
+# iterate.
+POLISH_RHO, POLISH_ITERS, POLISH_EQ, POLISH_FEAS = 1e10, 12, 1e-10, 1e-10
+
+
+def al_polish(A, Bm, xbar, ubar, xref, uref, spec, dx, du, rows_u, rows_x, ok, rho=None, iters=None, diag=None):
+    """Augmented-Lagrangian polish of the box QP on the interior point's active set (see above).
+    rows_u / rows_x = (y, lb, ub, s_l, s_u, lambda_l, lambda_u) of the input rows (stages 0..N-1)
+    and the state rows (stages 1..N-1).  Returns the polished (dx, du) and the per-instance
+    acceptance flag (False where ``ok`` is False)."""
+    rho = POLISH_RHO if rho is None else rho
+    iters = POLISH_ITERS if iters is None else iters
+    Bsz, N = xbar.shape[0], spec.N
+    NX = A.shape[-1]
+
+    def classify(y, lb, ub, sl, su, ll, lu):
+        side = np.where(ll > sl, -1.0, np.where(lu > su, 1.0, 0.0))
+        return side, np.where(side != 0, lu - ll, 0.0)
+
+    su_, nu_u = classify(*rows_u)
+    sx_, nu_x = classify(*rows_x)
+    yu0, yx0 = rows_u[0], rows_x[0]
+    (lbu, ubu), (lbx, ubx) = rows_u[1:3], rows_x[1:3]
+    zgap = np.zeros((Bsz, N, NX))
+    zdx0 = np.zeros((Bsz, NX))
+    Qd = np.zeros((Bsz, N, NX))
+    qd = np.zeros((Bsz, N, NX))
+    okp = ok.copy()
+    done = np.zeros(Bsz, dtype=bool)
+    pdx, pdu = np.zeros_like(dx), np.zeros_like(du)
+    passes = np.zeros(Bsz, dtype=np.int32)
+    g3 = ok[:, None, None]
+    for _ in range(iters):
+        act3 = (okp & ~done)[:, None, None]
+        bu, bx = np.where(su_ < 0, lbu, ubu), np.where(sx_ < 0, lbx, ubx)
+        Rd = np.where(g3 & (su_ != 0), rho, 0.0)
+        rd = np.where(g3 & (su_ != 0), nu_u + rho * (yu0 - bu), 0.0)
+        Qd[:, 1:N] = np.where(g3 & (sx_ != 0), rho, 0.0)
+        qd[:, 1:N] = np.where(g3 & (sx_ != 0), nu_x + rho * (yx0 - bx), 0.0)
+        ddx, dd, _, ok2 = riccati_solve(A, Bm, zgap, zdx0, xbar + np.where(g3, dx, 0.0),
+                                        ubar + np.where(g3, du, 0.0), xref, uref, spec,
+                                        Rd=Rd, rd=rd, Qd=Qd, qd=qd)
+        fin = np.isfinite(ddx).all(axis=(1, 2)) & np.isfinite(dd).all(axis=(1, 2))
+        okp &= (ok2 & fin) | done
+        act3 = (okp & ~done)[:, None, None]
+        pdx, pdu = np.where(act3, ddx, pdx), np.where(act3, dd, pdu)
+        passes += (okp & ~done)
+        yu, yx = yu0 + dd, yx0 + ddx[:, 1:N]
+        eu, ex = np.where(su_ != 0, yu - bu, 0.0), np.where(sx_ != 0, yx - bx, 0.0)
+        nun_u, nun_x = nu_u + rho * eu, nu_x + rho * ex
+        eq = np.maximum(np.abs(eu).max(axis=(1, 2)), np.abs(ex).max(axis=(1, 2)))
+
+        # one change per pass (a primal active-set step): release the active row whose multiplier
+        # is the most negative once signed, else fix the inactive row furthest outside its bound
+        wu, wx = np.where(su_ != 0, su_ * nun_u, np.inf), np.where(sx_ != 0, sx_ * nun_x, np.inf)
+        vu = np.where(su_ == 0, np.maximum(lbu - yu, yu - ubu), -np.inf)
+        vx = np.where(sx_ == 0, np.maximum(lbx - yx, yx - ubx), -np.inf)
+        wmin = np.minimum(wu.min(axis=(1, 2)), wx.min(axis=(1, 2)))
+        vmax = np.maximum(vu.max(axis=(1, 2)), vx.max(axis=(1, 2)))
+        rel = wmin < 0
+        add = ~rel & (vmax > POLISH_FEAS)
+        conv = ~rel & ~add & (eq <= POLISH_EQ)
+        live = okp & ~done
+        if diag is not None:
+            diag.setdefault('trace', []).append((eq.copy(), wmin.copy(), vmax.copy()))
+        nu_u, nu_x = np.where(live[:, None, None] & (su_ != 0), nun_u, nu_u), np.where(live[:, None, None] & (sx_ != 0), nun_x, nu_x)
+        for b in np.nonzero(live & (rel | add))[0]:
+            if rel[b]:
+                if wu[b].min() <= wx[b].min():
+                    j = np.unravel_index(np.argmin(wu[b]), wu[b].shape)
+                    su_[b][j], nu_u[b][j] = 0.0, 0.0
+                else:
+                    j = np.unravel_index(np.argmin(wx[b]), wx[b].shape)
+                    sx_[b][j], nu_x[b][j] = 0.0, 0.0
+            else:
+                if vu[b].max() >= vx[b].max():
+                    j = np.unravel_index(np.argmax(vu[b]), vu[b].shape)
+                    su_[b][j], nu_u[b][j] = (-1.0 if yu[b][j] < lbu[b][j] else 1.0), 0.0
+                else:
+                    j = np.unravel_index(np.argmax(vx[b]), vx[b].shape)
+                    sx_[b][j], nu_x[b][j] = (-1.0 if yx[b][j] < lbx[b][j] else 1.0), 0.0
+        done |= okp & conv
+        if not (okp & ~done).any():
+            break
+    acc = done & okp
+    if diag is not None:   # diagnostics (tools, tests)
+        diag.update(passes=passes, done=done, okp=okp, n_act=(su_ != 0).sum(axis=(1, 2)) + (sx_ != 0).sum(axis=(1, 2)))
+    return dx + pdx, du + pdu, acc
 
 
 def mpc_solve(x0, xref, uref, spec: OcpSpec, wind=None, mode='rollout', xbar=None, ubar=None,

@@ -261,10 +261,10 @@ def _sbox_inputs(B, N, seed):
 @pytest.mark.parametrize('mode', ['rollout', 'iterate'])
 def test_solve17_state_box_matches_oracle_interior_point(mode):
     """The reference's state box (JSON idxbx, stages 1..N-1) with its input box: the device
-    interior point equals the oracle's iteration (<= 1e-6: both stop at the conditioning limit
-    near the solution, mu ~ 1e-12 with lambda / s ~ 1e16 on active rows, where the iterate is
-    determined to ~1e-7 and one more or fewer step shows) and carries a KKT certificate of the
-    condensed QP (oracle.ocp.dense_kkt_certificate: NNLS multipliers >= 0, stationarity,
+    interior point and its active-set polish (oracle.ocp.al_polish) equal the oracle's (<= 1e-9:
+    the polished point is the exact solution of the equality-constrained QP on the active set, so
+    the two no longer differ by where each interior point stopped) and carry a KKT certificate of
+    the condensed QP (oracle.ocp.dense_kkt_certificate: NNLS multipliers >= 0, stationarity,
     feasibility, and a duality gap that bounds the suboptimality)."""
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     from oracle.ocp import dense_kkt_certificate
@@ -297,8 +297,12 @@ def test_solve17_state_box_matches_oracle_interior_point(mode):
     print(f'17/6 state box fp64 {mode}: u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e} vs oracle; KKT certificate: '
           f'stationarity {stat.max():.1e} violation {viol.max():.1e} duality gap {gap.max():.1e}; '
           f'{n_act} active state rows, oracle iterations max {o["iters"].max()}')
-    assert max(e) <= 1e-6
-    assert stat.max() <= 1e-8 and viol.max() <= 1e-9 and gap.max() <= 1e-5
+    assert max(e) <= 1e-9
+    assert stat.max() <= 1e-10 and viol.max() <= 1e-10 and gap.max() <= 1e-5
+    # the kernel's own count of interior-point iterations and polish passes (mpcb_qp_stats)
+    qs = m.qp_stats(B).cpu().numpy()
+    print(f'   device iterations {qs[:, 0].tolist()} oracle {o["iters"].tolist()}; polish passes {qs[:, 1].tolist()}')
+    assert (np.abs(qs[:, 0] - o['iters']) <= 1).all() and (qs[:, 1] >= 1).all()
 
 
 def test_solve17_state_box_infeasible_instances_flagged():
@@ -325,20 +329,22 @@ def test_solve17_state_box_infeasible_instances_flagged():
     assert (~feas).any() and feas.sum() >= B // 2
     assert np.array_equal(st == 0, feas) and np.array_equal(o['status'] == 0, feas)
     assert (st[~feas] == 4).all()
-    # the feasible ones: near-degenerate instances are determined only to ~1e-5 (2.3e-5 measured) at the
-    # conditioning limit where both iterations stop, so the KKT certificate is the sharp check
+    # the feasible ones: the polish takes both interior points (which stop up to an iteration apart
+    # at the conditioning limit on near-degenerate instances: 2.3e-5 apart in u0 before it) to the
+    # same exact active-set solution
     from oracle.ocp import dense_kkt_certificate
     ok = feas
     U = m.get_input_trajectory().cpu().numpy()
     e_u0 = relerr(m.get_control().cpu().numpy()[ok], o["u0"][ok]).max()
-    print(f"feasible instances: u0 vs oracle {e_u0:.2e}")
-    assert e_u0 <= 1e-4
+    e_U = relerr(U[ok], o['U'][ok]).max()
+    print(f"feasible instances: u0 vs oracle {e_u0:.2e}, U {e_U:.2e}")
+    assert e_u0 <= 1e-8 and e_U <= 1e-8
     stat, viol, gap = dense_kkt_certificate(o['A'][ok], o['B'][ok], o['gap'][ok], (x0 - o['xbar'][:, 0])[ok],
                                             o['xbar'][ok], o['ubar'][ok], np.broadcast_to(xref, (B, N + 1, 17))[ok],
                                             np.broadcast_to(uref, (B, N, 6))[ok], spec, (U - o['ubar'])[ok],
                                             lbx=lbx, ubx=ubx)
     # (gap bounds f(z) - f*; the objectives are ~1e3 here, so 1e-4 is 1e-7 relative)
-    assert stat.max() <= 1e-8 and viol.max() <= 1e-9 and gap.max() <= 1e-4, (stat.max(), viol.max(), gap.max())
+    assert stat.max() <= 1e-10 and viol.max() <= 1e-10 and gap.max() <= 1e-4, (stat.max(), viol.max(), gap.max())
 
 
 def test_full17_phase_timing_events():
@@ -494,9 +500,10 @@ def test_full_size_17_input_box_properties():
 def test_solve17_state_box_thin_interior_instance_converges():
     """LP-feasible state-box QPs whose Riccati recursion loses positive definiteness before
     mu = 1e-8 (tests/golden/sbox_thin_interior.npz, tools/make_sbox_fixture.py; lambda / s ~ 1e16
-    on strongly active rows).  They used to end QP_FAIL (the breakdown tolerance was 1e-8); they
-    converge now, on the device as in the oracle, with u0 near the oracle's and a KKT
-    certificate."""
+    on strongly active rows).  Both interior points stop at that limit (the device on the second
+    instance one iteration before the oracle: mu 1.3e-6 against 6.6e-8, u0 2.4e-5 apart); the
+    polish then finds the active set (on the second instance it releases the three rows the ratio
+    test took wrongly) and both end at its exact solution, with a KKT certificate."""
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     from oracle.ocp import dense_kkt_certificate
     d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'sbox_thin_interior.npz'))
@@ -523,9 +530,5 @@ def test_solve17_state_box_thin_interior_instance_converges():
     print(f'17/6 thin-interior state box: device status {st}, oracle {o["status"]} after {o["iters"]} iterations; '
           f'u0 {e:.2e} vs oracle; KKT stationarity {stat.max():.1e} violation {viol.max():.1e} gap {gap.max():.1e}')
     assert (o['status'] == 0).all() and (st == 0).all()
-    # both stop where the Newton system breaks (lambda / s ~ 1e16), the device on the second
-    # instance one iteration before the oracle (mu 1.3e-6 against 6.6e-8): the iterate there is
-    # determined to ~1e-5 (u0 2.4e-5 from the oracle's measured), and its KKT certificate reads
-    # stationarity 1.8e-5 and duality gap 4.6e-4 (1.3e-7 and 7.6e-6 on the first instance)
-    assert e <= 1e-4
-    assert stat.max() <= 1e-4 and viol.max() <= 1e-9 and gap.max() <= 1e-3
+    assert e <= 1e-7   # north_star 1e-5; measured 4.6e-9
+    assert stat.max() <= 1e-10 and viol.max() <= 1e-10 and gap.max() <= 1e-6

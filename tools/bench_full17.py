@@ -74,6 +74,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     bad = int((outs[3] != 0).sum().item())
+    status_counts = np.bincount(outs[3].cpu().numpy(), minlength=5).tolist()   # OK, NAN, MAXITER, MINSTEP, QP_FAIL
     m.set_timing(True)                     # one more solve with per-phase HIP events
     m.solve(x0t, xrt, urt, out=outs)
     ph = m.last_timing()
@@ -83,27 +84,51 @@ def main():
     # P update 2 nx^2 nu, vector terms 2 nx^2 + 2 nz nx + 2 (nx^2 + nu^2) + 2 nx nu, and the
     # forward pass 2 nu nx + 2 nx nz
     nx_, nu_, nz_ = 17, 6, 23
+    fwd = 2 * nu_ * nx_ + 2 * nx_ * nz_
     fl = (2 * nx_ * nx_ * nz_ + 2 * nz_ * nz_ * nx_ + nu_ ** 3 / 3 + 2 * nu_ * nu_ * (nx_ + 1) + 2 * nx_ * nx_ * nu_
-          + 2 * nx_ * nx_ + 2 * nz_ * nx_ + 2 * (nx_ * nx_ + nu_ * nu_) + 2 * nx_ * nu_ + 2 * nu_ * nx_ + 2 * nx_ * nz_)
+          + 2 * nx_ * nx_ + 2 * nz_ * nx_ + 2 * (nx_ * nx_ + nu_ * nu_) + 2 * nx_ * nu_ + fwd)
     peak = 78.6 if args.dtype == 'f64' else 157.3
-    roof = None
-    if args.bounds == 'none':
-        # the 16-lane DPP kernel (mpcb_r17.hip) unless MPCB_R17=0; dense count over the kernel's
-        # HIP-event time; executed_frac from the committed PMC summary (profiles/pmc_full17.json,
-        # 64 x SQ_INSTS_VALU_FLOPS_FP64 per launch: the kernel skips the 9 structural columns)
-        q17 = os.environ.get('MPCB_R17', '1') != '0'
-        kname = ('q17::riccati17q_kernel' if q17 else 'riccati17_kernel') + f'<{"double" if args.dtype == "f64" else "float"}, false>'
-        ach = fl * N * B / (ph['riccati'] * 1e-3) / 1e12
-        ex = None
-        pj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_full17.json')
-        if os.path.exists(pj) and args.dtype == 'f64' and B == 4096 and N == 60:
-            e = json.load(open(pj)).get('per_kernel', {}).get('mpcb::' + kname, {}).get('executed_flops_per_launch')
-            ex = e / (ph['riccati'] * 1e-3) / 1e12 / peak if e else None
-        roof = {'bound': 'valu', 'kernel': kname, 'flop_per_stage': fl, 'achieved': ach,
-                'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak, 'executed_frac': ex}
+    t = 'double' if args.dtype == 'f64' else 'float'
+    box = args.bounds != 'none'
+    meh = args.bounds == 'input' and args.dtype == 'f64'
+    kname = f'q17::riccati17q_kernel<{t}, {"true" if box else "false"}, {"true" if meh else "false"}>'
+    # interior point (boxes): per iteration one Riccati backward with the row terms and one forward
+    # step (fl per stage), plus the rows' step-length and update arithmetic (~12 flop per row and
+    # pass: rows = nu + nx with the state box); Mehrotra adds its affine step and a vector-only
+    # corrector pass (the h_u, k, p' recursion over the stored factor: 2 nz nx + 2 nu^2 + 2 nx nu
+    # + 2 nu nx) and the corrector's forward.  The polish pass (state box) is one backward +
+    # forward + a row pass.  Iterations and polish passes are counted per instance by the kernel
+    # (mpcb_qp_stats), so the count is the work each instance needed, not the wave's lock-step.
+    rows = nu_ + (nx_ if args.bounds == 'all' else 0)
+    it_fl = fl + 2 * 12 * rows + ((2 * nz_ * nx_ + 2 * nu_ * nu_ + 4 * nx_ * nu_ + fwd) if meh else 0)
+    pol_fl = fl + 12 * rows
+    qp = None
+    if box:
+        st = m.qp_stats(B).double().cpu().numpy()
+        qp = dict(mean_iters=float(st[:, 0].mean()), max_iters=int(st[:, 0].max()),
+                  mean_polish=float(st[:, 1].mean()), max_polish=int(st[:, 1].max()),
+                  iters_total=float(st[:, 0].sum()), polish_total=float(st[:, 1].sum()))
+        flop = (it_fl * qp['iters_total'] + pol_fl * qp['polish_total']) * N
+    else:
+        flop = fl * N * B
+    ach = flop / (ph['riccati'] * 1e-3) / 1e12
+    # executed flops from the committed PMC summary (profiles/pmc_full17*.json, per dispatch = one
+    # launch here: 64 x SQ_INSTS_VALU_FLOPS_FP64) at the profiled configuration
+    ex = None
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pj = os.path.join(root, 'profiles', 'pmc_full17.json' if not box else f'pmc_full17_{args.bounds}.json')
+    if os.path.exists(pj) and args.dtype == 'f64' and B == 4096 and N == 60:
+        e = json.load(open(pj)).get('per_kernel', {}).get('mpcb::' + kname, {}).get('executed_flops_per_launch')
+        ex = e / (ph['riccati'] * 1e-3) / 1e12 / peak if e else None
+    roof = {'bound': 'valu', 'kernel': kname, 'flop_per_stage': fl, 'flop_per_launch': flop,
+            'achieved': ach, 'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak, 'executed_frac': ex,
+            'kernel_ms': ph['riccati']}
+    if qp:
+        roof.update(interior_point=qp, flop_per_iteration_stage=it_fl, flop_per_polish_stage=pol_fl)
     print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
                       'unit': 'solves/s', 'ms_per_step': el / args.steps * 1e3, 'batch': B,
-                      'dtype': args.dtype, 'bad_status': bad, 'bounds': args.bounds,
+                      'dtype': args.dtype, 'bad_status': bad, 'status_counts': status_counts,
+                      'bounds': args.bounds,
                       'phase_ms': ph, 'roofline': roof,
                       'config': 'reference OCP (acados_ocp_blasterModel.json), random x0 + POC params'}))
 
