@@ -323,7 +323,7 @@ constexpr double IPM17_SIGMA_MIN = 0.05, IPM17_SIGMA_MAX = 0.9, IPM17_TAU = 0.99
 constexpr double IPM17_TOL = 1e-12, IPM17_BREAK = 1e-5, IPM17_STALL = 1e-6, IPM17_RES = 1e-9;
 // the fp64 state-box polish (oracle.ocp.al_polish): augmented-Lagrangian passes over the
 // interior point's active set with one active-set change per pass
-constexpr double POL17_RHO = 1e10, POL17_EQ = 1e-10, POL17_FEAS = 1e-10;
+constexpr double POL17_RHO = 1e10, POL17_EQ = 1e-10, POL17_FEAS = 1e-10, POL17_ACT = 100.0;
 constexpr int POL17_ITERS = 12;
 constexpr double IPM17_SHORT = 1e-2;   // IPM17_SHORT_RUN steps in a row below it: a stalled QP
 constexpr int IPM17_SHORT_RUN = 10;

@@ -909,9 +909,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     int pst = 0, npass = 0, nit = 0;   // (nit: this group's interior-point iterations)
     bool early = false;    // stopped at the conditioning limit (breakdown / collapsed step)
     const int it_max = a.max_as_iter + (polish ? POL17_ITERS : 0);
-    auto classify = [&]() {   // side = -1 (lower) / +1 (upper) / 0, nu = lambda_u - lambda_l
+    auto classify = [&]() {   // side = -1 (lower) / +1 (upper) / 0 by lambda > 100 s, nu = lambda_u - lambda_l
       auto cl = [&](T sl, T su, T ll, T lu, T& nu, T& side) {
-        side = ll > sl ? T(-1) : (lu > su ? T(1) : T(0));
+        side = ll > T(POL17_ACT) * sl ? T(-1) : (lu > T(POL17_ACT) * su ? T(1) : T(0));
         nu = side != T(0) ? lu - ll : T(0);
       };
       if (in) {

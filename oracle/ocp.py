@@ -616,22 +616,23 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
 
 # The polish after the state-box interior point (HPIPM's analogue: its final "exact" step on the
 # identified active set).  At the interior point's last iterate a row is taken as active on its
-# lower side when lambda_l > s_l (upper likewise): on a strongly active row lambda / s ~ 1e4..1e16,
-# on an inactive one ~1e-2 or less.  The equality-constrained QP on that active set is solved by the
+# lower side when lambda_l > POLISH_ACT s_l (upper likewise): on a strongly active row lambda / s ~
+# 1e4..1e16, on an inactive one ~1e-2 or less; the rows in between (lambda ~ s ~ sqrt(mu): weakly
+# active, degenerate) are left free at first.  (With the midpoint ratio 1, 33 of the 4096 bench
+# draws took such rows into mutually inconsistent sets, whose multipliers then run off and the
+# pass cap ended the polish; with 100 every LP-feasible draw instance is polished in <= 4 passes.)  The equality-constrained QP on that active set is solved by the
 # method of multipliers over the same Riccati recursion: each pass is one linear solve, the
 # minimiser of the augmented Lagrangian  J + nu'(Cz - b) + rho/2 |Cz - b|^2  (diagonal rho on the
 # active rows, gradient nu + rho (y - b): the interior point's D / d slots), linearised at the
 # interior point's iterate z0 (the QP is quadratic, so the minimiser does not depend on it), then
-# nu <- nu + rho (y - b).  nu starts at lambda_u - lambda_l.  Near the conditioning limit the ratio
-# test can take a row that is not active at the solution (the thin-interior fixture: 2 of 356 rows,
-# whose equalities are then inconsistent with the others and whose multipliers run off with the
-# wrong sign), so every pass also corrects the set as a primal-dual active-set step would: an
-# active row whose multiplier has the wrong sign is released (nu = 0), an inactive row outside its
-# bound is fixed at it (nu = 0).  An instance is done when its set did not change and every active
-# row is within POLISH_EQ of its bound; it then keeps the polished point if the Riccati recursion
-# stayed positive definite.  An instance not done after POLISH_ITERS passes keeps the interior-point
-# iterate.
+# nu <- nu + rho (y - b).  nu starts at lambda_u - lambda_l.  Every pass also corrects the set by
+# one primal active-set step: the active row whose multiplier is the most negative once signed is
+# released (nu = 0), else the inactive row furthest outside its bound is fixed at it (nu = 0).  An
+# instance is done when its set did not change and every active row is within POLISH_EQ of its
+# bound; it then keeps the polished point if the Riccati recursion stayed positive definite.  An
+# instance not done after POLISH_ITERS passes keeps the interior-point iterate.
 POLISH_RHO, POLISH_ITERS, POLISH_EQ, POLISH_FEAS = 1e10, 12, 1e-10, 1e-10
+POLISH_ACT = 100.0   # a row is active when lambda > 100 s (ratio 1 takes ambiguous rows: inconsistent sets)
 
 
 def al_polish(A, Bm, xbar, ubar, xref, uref, spec, dx, du, rows_u, rows_x, ok, rho=None, iters=None, diag=None):
@@ -645,7 +646,7 @@ def al_polish(A, Bm, xbar, ubar, xref, uref, spec, dx, du, rows_u, rows_x, ok, r
     NX = A.shape[-1]
 
     def classify(y, lb, ub, sl, su, ll, lu):
-        side = np.where(ll > sl, -1.0, np.where(lu > su, 1.0, 0.0))
+        side = np.where(ll > POLISH_ACT * sl, -1.0, np.where(lu > POLISH_ACT * su, 1.0, 0.0))
         return side, np.where(side != 0, lu - ll, 0.0)
 
     su_, nu_u = classify(*rows_u)
