@@ -3,11 +3,14 @@
 Same signature and call sequence as the reference:
 ``blasterModel(mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
 controlBound)``, ``.generateModel()``, ``.generateController() -> (integrator, ocp_solver)``.
-``full_model=True`` keeps the reference's 17/6 model, its weights, its input box (controlBound:
-thrusts and swivel rates) and its state box (statesBound, stages 1..N-1, blastermodel.py:268-270)
-unchanged — the device's 17/6 path; a statesBound with non-finite entries leaves the state box
-off.  The default keeps the 12/4 rigid-body slice of the BASELINE configs: Q[:12,:12], R[:4,:4],
-thrust bounds controlBound[:, :4]; there statesBound is accepted but not enforced.
+By default (``full_model=True``) it keeps the reference's 17/6 model, its weights, its input box
+(controlBound: thrusts and swivel rates) and its state box (statesBound, stages 1..N-1,
+blastermodel.py:268-270) unchanged — the device's 17/6 path, so swapping the import is all a
+reference script needs; a statesBound with non-finite entries leaves the state box off.
+``full_model=False`` selects the 12/4 rigid-body slice of the BASELINE configs: Q[:12,:12],
+R[:4,:4], thrust bounds controlBound[:, :4].  The slice has no state box: a finite statesBound
+there raises NotImplementedError at generateController (a silently unenforced constraint would
+change the reference's OCP).
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ DEFAULT_T_BLAST = 2.2 * 9.81
 class blasterModel:  # noqa: N801  (reference class name)
     def __init__(self, mass, J, l_x, l_y, N, Tf, c, Q, R, Q_t, blastThruster, statesBound,
                  controlBound, dtype: str = 'f64', batch: int = 1, device: int = 0,
-                 full_model: bool = False):
+                 full_model: bool = True):
         self._M = float(mass)
         self._J = np.asarray(J, dtype=np.float64)
         self._arm_length_x = float(l_x)
@@ -82,10 +85,11 @@ class blasterModel:  # noqa: N801  (reference class name)
     def generateController(self):
         if self._cfg is None:
             self.generateModel()
-        if not (self._full and self._cfg.lbx is not None) and self._statesBound.size and \
-                np.isfinite(self._statesBound).any():
-            warnings.warn('statesBound is not enforced by this build (stage state boxes are out of '
-                          'scope); x0 is pinned through set(0, "lbx"/"ubx")', stacklevel=2)
+        if not self._full and self._statesBound.size and np.isfinite(self._statesBound).any():
+            raise NotImplementedError(
+                'statesBound (blastermodel.py:268-270) on the 12/4 slice: the slice has no state box; '
+                'use full_model=True (the default: the reference 17/6 OCP with its state box) or pass '
+                'a non-finite statesBound')
         ocp = AcadosOcpSolver(self._cfg, batch=self._batch, device=self._device,
                               json_file='acados_ocp_blasterModel.json')
         sim = AcadosSimSolver(MPCConfig(**{**self._cfg.__dict__}), batch=self._batch,

@@ -113,3 +113,15 @@ def test_library_abi_version_is_checked_at_load(tmp_path):
     subprocess.check_call(['gcc', '-shared', '-fPIC', str(src), '-o', str(so)])
     with pytest.raises(_lib.LibraryMissing, match='ABI version 3'):
         _lib.load(str(so))
+
+
+def test_slice_refuses_a_finite_state_box():
+    """The 12/4 slice has no state box: the reference's finite statesBound raises there (instead of
+    being silently dropped); the default model is the reference's 17/6 OCP, which enforces it."""
+    b = blasterModel(*_reference_args(), full_model=False)
+    b.generateModel()
+    with pytest.raises(NotImplementedError, match='statesBound'):
+        b.generateController()
+    b2 = blasterModel(*_reference_args())
+    b2.generateModel()
+    assert b2._cfg.nx == 17 and b2._cfg.lbx is not None

@@ -532,3 +532,33 @@ def test_solve17_state_box_thin_interior_instance_converges():
     assert (o['status'] == 0).all() and (st == 0).all()
     assert e <= 1e-7   # north_star 1e-5; measured 4.6e-9
     assert stat.max() <= 1e-10 and viol.max() <= 1e-10 and gap.max() <= 1e-5   # (gap: objective ~1e3)
+
+
+def test_closed_loop17_reference_ocp_matches_oracle():
+    """The receding-horizon loop of simulation_blaster.py:56-107 on the reference's own OCP
+    (acados_ocp_blasterModel.json: 17/6, N = 60, input box and state box, the JSON's parameters),
+    batched: B = 64 instances, 20 steps of SQP_RTI from the persistent iterate plus the plant step,
+    all on the device (mpc_blaster_amd.closed_loop) against the oracle's loop
+    (tests/golden/loop17_ref.npz, tools/make_loop17_fixture.py) at <= 1e-5 per step (north_star)."""
+    import warnings
+    from mpc_blaster_amd import BatchedMPC, load_acados_ocp_json
+    from mpc_blaster_amd.closed_loop import closed_loop
+    d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'loop17_ref.npz'))
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        cfg, info = load_acados_ocp_json(os.path.join(os.path.dirname(__file__), 'golden', 'ocp_json_pin.json'))
+    x0, nsim = d['x0'], int(d['nsim'])
+    B, N = x0.shape[0], cfg.N
+    m = BatchedMPC(cfg, max_batch=B)
+    m.set_params(np.tile(d['p'], (B, 1)))
+    xr = np.broadcast_to(d['xref'], (1, N + 1, 17))
+    ur = np.broadcast_to(d['uref'], (1, N, 6))
+    Xs, Us, st = closed_loop(m, x0, xr, ur, nsim)
+    torch.cuda.synchronize()
+    Xs, Us, st = Xs.cpu().numpy(), Us.cpu().numpy(), st.cpu().numpy()
+    eu = max(relerr(Us[:, i], d['Us'][:, i]).max() for i in range(nsim))
+    ex = max(relerr(Xs[:, i], d['Xs'][:, i]).max() for i in range(nsim + 1))
+    print(f'17/6 closed loop B={B} x {nsim} steps: u0 {eu:.2e} x {ex:.2e} vs oracle; statuses '
+          f'{np.bincount(d["status"].ravel(), minlength=5)} (oracle, all steps)')
+    assert np.array_equal(st, d['status'].max(axis=1))
+    assert eu <= 1e-5 and ex <= 1e-5

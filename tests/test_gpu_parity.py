@@ -370,7 +370,7 @@ def test_acados_facade_runs_reference_loop(t_blast):
     cb = np.array([[0, 0, 0, 0, -0.0872665, -0.0872665], [65, 65, 65, 65, 0.0872665, 0.0872665]])
     N = 15
     b = blasterModel(9.0, J, 0.3434, 0.3475, N, N / 30.0, 0.03, Q, R, 10 * Q, 0.0,
-                     np.full((2, 17), np.nan), cb)
+                     np.full((2, 17), np.nan), cb, full_model=False)
     b.generateModel()
     integrator, ocp_solver = b.generateController()
     x = np.zeros(17)

@@ -227,3 +227,18 @@ def test_polish_active_set_changes(monkeypatch):
     wmin = [t[1][0] for t in diag['trace']]
     assert min(wmin) < 0                                   # a release happened
     assert np.abs(o['U'] - ref['U']).max() <= 1e-7 * np.abs(ref['U']).max()
+
+
+def test_loop17_fixture_is_the_oracle_loop():
+    """tests/golden/loop17_ref.npz (the GPU closed-loop test's reference) is what the oracle's loop
+    gives: two instances, the first three steps, recomputed here."""
+    import importlib.util
+    spec_ = importlib.util.spec_from_file_location('mkloop', os.path.join(os.path.dirname(GOLD), '..', 'tools',
+                                                                        'make_loop17_fixture.py'))
+    mk = importlib.util.module_from_spec(spec_)
+    spec_.loader.exec_module(mk)
+    d = np.load(os.path.join(GOLD, 'loop17_ref.npz'))
+    Xs, Us, st, it = mk.run(np.array([0, 1]), nsim=3)
+    assert np.abs(Us - d['Us'][:2, :3]).max() <= 1e-12 * np.abs(d['Us']).max()
+    assert np.abs(Xs - d['Xs'][:2, :4]).max() <= 1e-12 * np.abs(d['Xs']).max()
+    assert np.array_equal(st, d['status'][:2, :3])
