@@ -8,6 +8,8 @@
  *   LINEAR_LS cost with stage scaling s = dt (blastermodel.py:228-257),
  *   Riccati recursion with symmetrised P, forward pass -> u0, X, U.
  * Dynamics: 12-state/4-input slice of f_expl_expr (blastermodel.py:95-201).
+ * Input box (c4, blastermodel.py:259-264): the primal-dual active set with the Kim-Park safeguard
+ * and Murty's least-index backup of oracle/ocp.py pdas_solve, over the masked Riccati recursion.
  * Parallel over instances with OpenMP (one instance per thread at a time).
  */
 #include <math.h>
@@ -24,7 +26,7 @@ typedef struct {
   double dt, s;
 } oracle_params;
 
-static void f_eval(const double* x, const double* u, const oracle_params* P, double* f, double* Jf /* NX x NZ or NULL */) {
+static void f_eval(const double* x, const double* u, const oracle_params* P, const double* w, double* f, double* Jf /* NX x NZ or NULL */) {
   const double sf = sin(x[3]), cf = cos(x[3]), st = sin(x[4]), ct = cos(x[4]), sp = sin(x[5]), cp = cos(x[5]);
   const double ict = 1.0 / ct, tt = st * ict;
   const double wx = x[9], wy = x[10], wz = x[11];
@@ -34,6 +36,7 @@ static void f_eval(const double* x, const double* u, const oracle_params* P, dou
   const double Tt = u[0] + u[1] + u[2] + u[3] + P->t_blast, s = Tt * P->minv;
   const double r0 = cp * cf * st + sp * sf, r1 = sp * cf * st - cp * sf, r2 = cf * ct;
   f[6] = r0 * s; f[7] = r1 * s; f[8] = r2 * s - P->g;
+  if (w) { f[6] += w[0] * P->minv; f[7] += w[1] * P->minv; f[8] += w[2] * P->minv; }   /* c5 wind force */
   const double* J = P->J;
   const double jw0 = J[0] * wx + J[1] * wy + J[2] * wz, jw1 = J[3] * wx + J[4] * wy + J[5] * wz,
                jw2 = J[6] * wx + J[7] * wy + J[8] * wz;
@@ -84,7 +87,7 @@ static void f_eval(const double* x, const double* u, const oracle_params* P, dou
 }
 
 /* x_next and S = [A | B] (NX x NZ, row-major) */
-static void rk4_sens(const double* x, const double* u, const oracle_params* P, double* xn, double* S) {
+static void rk4_sens(const double* x, const double* u, const oracle_params* P, const double* w, double* xn, double* S) {
   const double h = P->dt;
   double k[4][NX], dk[4][NX * NZ], xs[NX], Jf[NX * NZ], Ss[NX * NZ];
   double S0[NX * NZ];
@@ -94,7 +97,7 @@ static void rk4_sens(const double* x, const double* u, const oracle_params* P, d
   for (int st = 0; st < 4; ++st) {
     for (int i = 0; i < NX; ++i) xs[i] = st ? x[i] + c[st] * h * k[st - 1][i] : x[i];
     for (int i = 0; i < NX * NZ; ++i) Ss[i] = st ? S0[i] + c[st] * h * dk[st - 1][i] : S0[i];
-    f_eval(xs, u, P, k[st], Jf);
+    f_eval(xs, u, P, w, k[st], Jf);
     for (int i = 0; i < NX; ++i)
       for (int j = 0; j < NZ; ++j) {
         double acc = (j >= NX) ? Jf[i * NZ + j] : 0.0;
@@ -132,13 +135,13 @@ static int chol_solve4(const double* H, double* Bm /* NU x ncols, overwritten */
 }
 
 static int solve_one(int N, const oracle_params* P, const double* x0, const double* xr, const double* ur,
-                     double* u0, double* X, double* U, double* work) {
+                     const double* w, double* u0, double* X, double* U, double* work) {
   double* xb = work;                     /* (N+1) x NX */
   double* S = xb + (N + 1) * NX;         /* N x NX x NZ */
   double* K = S + N * NX * NZ;           /* N x NU x NX */
   double* kf = K + N * NU * NX;          /* N x NU */
   memcpy(xb, x0, sizeof(double) * NX);
-  for (int k = 0; k < N; ++k) rk4_sens(xb + k * NX, ur + k * NU, P, xb + (k + 1) * NX, S + k * NX * NZ);
+  for (int k = 0; k < N; ++k) rk4_sens(xb + k * NX, ur + k * NU, P, w, xb + (k + 1) * NX, S + k * NX * NZ);
   double Pm[NX * NX], p[NX], e[NX];
   memcpy(Pm, P->QN, sizeof Pm);
   for (int i = 0; i < NX; ++i) e[i] = xb[N * NX + i] - xr[N * NX + i];
@@ -216,10 +219,198 @@ static int solve_one(int N, const oracle_params* P, const double* x0, const doub
 
 #include <stdlib.h>
 
+/* ---- input box: oracle/ocp.py pdas_solve (rollout mode: ubar = uref, zero gaps, dx_0 = 0) ---- */
+typedef struct { double lbu[NU], ubu[NU]; int max_iter, pbar; } box_params;
+
+/* One masked Riccati pass + forward pass with multipliers (oracle/ocp.py riccati_solve with
+ * fixed / delta): fixed inputs du = delta, the others free.  Writes du, dx, mu; returns 0 or 4. */
+static int masked_pass(int N, const oracle_params* P, const double* xb, const double* S, const double* xr,
+                       const double* ur, const unsigned char* fixed, const double* delta, double* K,
+                       double* kf, double* Huus, double* Huxs, double* hus, double* dx, double* du,
+                       double* mu) {
+  double Pm[NX * NX], p[NX], e[NX];
+  memcpy(Pm, P->QN, sizeof Pm);
+  for (int i = 0; i < NX; ++i) e[i] = xb[N * NX + i] - xr[N * NX + i];
+  for (int i = 0; i < NX; ++i) { double acc = 0; for (int j = 0; j < NX; ++j) acc += P->QN[i * NX + j] * e[j]; p[i] = acc; }
+  for (int k = N - 1; k >= 0; --k) {
+    const double* Sk = S + k * NX * NZ;
+    double PS[NX * NZ], H[NZ * NZ], h[NZ];
+    for (int i = 0; i < NX; ++i)
+      for (int j = 0; j < NZ; ++j) { double acc = 0; for (int l = 0; l < NX; ++l) acc += Pm[i * NX + l] * Sk[l * NZ + j]; PS[i * NZ + j] = acc; }
+    for (int i = 0; i < NZ; ++i)
+      for (int j = 0; j < NZ; ++j) { double acc = 0; for (int l = 0; l < NX; ++l) acc += Sk[l * NZ + i] * PS[l * NZ + j]; H[i * NZ + j] = acc; }
+    for (int j = 0; j < NZ; ++j) { double acc = 0; for (int l = 0; l < NX; ++l) acc += Sk[l * NZ + j] * p[l]; h[j] = acc; }
+    for (int i = 0; i < NX; ++i) e[i] = xb[k * NX + i] - xr[k * NX + i];
+    for (int i = 0; i < NX; ++i) {
+      double acc = 0;
+      for (int j = 0; j < NX; ++j) { H[i * NZ + j] += P->s * P->Q[i * NX + j]; acc += P->Q[i * NX + j] * e[j]; }
+      h[i] += P->s * acc;
+    }
+    for (int m = 0; m < NU; ++m)
+      for (int n = 0; n < NU; ++n) H[(NX + m) * NZ + NX + n] += P->s * P->R[m * NU + n];   /* ubar = uref */
+    double* Huu = Huus + k * NU * NU;
+    double* Hux = Huxs + k * NU * NX;
+    double* hu = hus + k * NU;
+    for (int m = 0; m < NU; ++m) {
+      for (int n = 0; n < NU; ++n) Huu[m * NU + n] = H[(NX + m) * NZ + NX + n];
+      for (int i = 0; i < NX; ++i) Hux[m * NX + i] = H[(NX + m) * NZ + i];
+      hu[m] = h[NX + m];
+    }
+    /* the masked stage (oracle/ocp.py _masked_stage) */
+    const unsigned char* fk = fixed + k * NU;
+    const double* dk = delta + k * NU;
+    double Ht[16], rhs[NU * (NX + 1)];
+    for (int m = 0; m < NU; ++m) {
+      double ht = hu[m];
+      for (int n = 0; n < NU; ++n) ht += fk[n] ? Huu[m * NU + n] * dk[n] : 0.0;
+      for (int n = 0; n < NU; ++n) Ht[m * NU + n] = (fk[m] || fk[n]) ? (m == n ? 1.0 : 0.0) : Huu[m * NU + n];
+      for (int i = 0; i < NX; ++i) rhs[m * (NX + 1) + i] = fk[m] ? 0.0 : -Hux[m * NX + i];
+      rhs[m * (NX + 1) + NX] = fk[m] ? dk[m] : -ht;
+    }
+    if (chol_solve4(Ht, rhs, NX + 1)) return 4;
+    for (int m = 0; m < NU; ++m) {
+      for (int i = 0; i < NX; ++i) K[(k * NU + m) * NX + i] = rhs[m * (NX + 1) + i];
+      kf[k * NU + m] = rhs[m * (NX + 1) + NX];
+    }
+    double Pn[NX * NX];
+    for (int i = 0; i < NX; ++i)
+      for (int j = 0; j < NX; ++j) {
+        double acc = H[i * NZ + j];
+        for (int m = 0; m < NU; ++m) acc += Hux[m * NX + i] * K[(k * NU + m) * NX + j];
+        Pn[i * NX + j] = acc;
+      }
+    for (int i = 0; i < NX; ++i)
+      for (int j = 0; j < NX; ++j) Pm[i * NX + j] = 0.5 * (Pn[i * NX + j] + Pn[j * NX + i]);
+    for (int i = 0; i < NX; ++i) {
+      double acc = h[i];
+      for (int m = 0; m < NU; ++m) acc += Hux[m * NX + i] * kf[k * NU + m];
+      p[i] = acc;
+    }
+  }
+  memset(dx, 0, sizeof(double) * NX);
+  for (int k = 0; k < N; ++k) {
+    const double* xk = dx + k * NX;
+    double* uk = du + k * NU;
+    for (int m = 0; m < NU; ++m) {
+      double acc = kf[k * NU + m];
+      for (int i = 0; i < NX; ++i) acc += K[(k * NU + m) * NX + i] * xk[i];
+      uk[m] = acc;
+    }
+    for (int m = 0; m < NU; ++m) {
+      double acc = hus[k * NU + m];
+      for (int n = 0; n < NU; ++n) acc += Huus[k * NU * NU + m * NU + n] * uk[n];
+      for (int i = 0; i < NX; ++i) acc += Huxs[k * NU * NX + m * NX + i] * xk[i];
+      mu[k * NU + m] = acc;
+    }
+    const double* Sk = S + k * NX * NZ;
+    for (int i = 0; i < NX; ++i) {
+      double acc = 0;
+      for (int j = 0; j < NX; ++j) acc += Sk[i * NZ + j] * xk[j];
+      for (int m = 0; m < NU; ++m) acc += Sk[i * NZ + NX + m] * uk[m];
+      dx[(k + 1) * NX + i] = acc;
+    }
+  }
+  return 0;
+}
+
+static int solve_one_box(int N, const oracle_params* P, const box_params* bp, const double* x0, const double* xr,
+                         const double* ur, double* u0, double* X, double* U, int* iters, double* work,
+                         unsigned char* flags) {
+  double* xb = work;                     /* (N+1) x NX */
+  double* S = xb + (N + 1) * NX;         /* N x NX x NZ */
+  double* K = S + N * NX * NZ;           /* N x NU x NX */
+  double* kf = K + N * NU * NX;          /* N x NU */
+  double* Huus = kf + N * NU;            /* N x NU x NU */
+  double* Huxs = Huus + N * NU * NU;     /* N x NU x NX */
+  double* hus = Huxs + N * NU * NX;      /* N x NU */
+  double* dx = hus + N * NU;             /* (N+1) x NX */
+  double* du = dx + (N + 1) * NX;        /* N x NU */
+  double* mu = du + N * NU;              /* N x NU */
+  double* delta = mu + N * NU;           /* N x NU */
+  unsigned char* low = flags;            /* N x NU */
+  unsigned char* up = low + N * NU;
+  unsigned char* fixed = up + N * NU;
+  unsigned char* V = fixed + N * NU;
+  memcpy(xb, x0, sizeof(double) * NX);
+  for (int k = 0; k < N; ++k) rk4_sens(xb + k * NX, ur + k * NU, P, NULL, xb + (k + 1) * NX, S + k * NX * NZ);
+  memset(low, 0, 2 * N * NU);
+  int best = 0x7fffffff, pcount = bp->pbar, done = 0, st = 0, it;
+  for (it = 0; it < bp->max_iter; ++it) {
+    for (int e = 0; e < N * NU; ++e) {
+      const int m = e % NU;
+      fixed[e] = low[e] | up[e];
+      delta[e] = low[e] ? bp->lbu[m] - ur[e] : (up[e] ? bp->ubu[m] - ur[e] : 0.0);
+    }
+    if (masked_pass(N, P, xb, S, xr, ur, fixed, delta, K, kf, Huus, Huxs, hus, dx, du, mu)) { st = 4; ++it; break; }
+    int nV = 0, first = -1;
+    for (int e = 0; e < N * NU; ++e) {
+      const int m = e % NU;
+      const double u = ur[e] + du[e];
+      V[e] = 0;
+      if (!fixed[e] && u < bp->lbu[m]) V[e] = 1;          /* v_lo */
+      else if (!fixed[e] && u > bp->ubu[m]) V[e] = 2;     /* v_hi */
+      else if (low[e] && mu[e] < 0) V[e] = 3;             /* v_fl */
+      else if (up[e] && mu[e] > 0) V[e] = 4;              /* v_fu */
+      if (V[e]) { ++nV; if (first < 0) first = e; }
+    }
+    if (nV == 0) { done = 1; ++it; break; }
+    const int full = (nV < best) || (pcount > 0);
+    pcount = (nV < best) ? bp->pbar : (full ? pcount - 1 : pcount);
+    if (nV < best) best = nV;
+    for (int e = 0; e < N * NU; ++e) {
+      if (!V[e] || (!full && e != first)) continue;
+      if (V[e] == 1) low[e] = 1;
+      else if (V[e] == 2) up[e] = 1;
+      else if (V[e] == 3) low[e] = 0;
+      else up[e] = 0;
+    }
+  }
+  if (!st && !done) st = 2;
+  *iters = it;
+  for (int k = 0; k <= N; ++k)
+    if (X) for (int i = 0; i < NX; ++i) X[k * NX + i] = xb[k * NX + i] + dx[k * NX + i];
+  for (int k = 0; k < N; ++k)
+    if (U) for (int m = 0; m < NU; ++m) U[k * NU + m] = ur[k * NU + m] + du[k * NU + m];
+  for (int m = 0; m < NU; ++m) u0[m] = ur[m] + du[m];
+  return st;
+}
+
+/* Input-box rollout-mode solve (BASELINE c4) for B instances; returns the number of non-OK ones. */
+int mpc_oracle_solve_box(int B, int N, const oracle_params* P, const double* lbu, const double* ubu,
+                         int max_iter, const double* x0, const double* xref, long xref_sb,
+                         const double* uref, long uref_sb, double* u0, double* X, double* U,
+                         int* status, int* iters, int nthreads) {
+  box_params bp;
+  memcpy(bp.lbu, lbu, sizeof bp.lbu);
+  memcpy(bp.ubu, ubu, sizeof bp.ubu);
+  bp.max_iter = max_iter;
+  bp.pbar = 3;
+  int bad = 0;
+  const size_t wsz = (size_t)(N + 1) * NX * 2 + (size_t)N * (NX * NZ + NU * NX * 2 + NU * NU + NU * 5);
+#pragma omp parallel num_threads(nthreads) reduction(+ : bad)
+  {
+    double* work = (double*)malloc(sizeof(double) * wsz);
+    unsigned char* flags = (unsigned char*)malloc((size_t)4 * N * NU);
+#pragma omp for schedule(dynamic, 16)
+    for (int b = 0; b < B; ++b) {
+      int it = 0;
+      int st = solve_one_box(N, P, &bp, x0 + (size_t)b * NX, xref + (size_t)b * xref_sb, uref + (size_t)b * uref_sb,
+                             u0 + (size_t)b * NU, X ? X + (size_t)b * (N + 1) * NX : NULL,
+                             U ? U + (size_t)b * N * NU : NULL, &it, work, flags);
+      if (status) status[b] = st;
+      if (iters) iters[b] = it;
+      bad += st != 0;
+    }
+    free(flags);
+    free(work);
+  }
+  return bad;
+}
+
 /* Unconstrained rollout-mode solve for B instances; returns the number of failed instances. */
 int mpc_oracle_solve(int B, int N, const oracle_params* P, const double* x0, const double* xref,
-                     long xref_sb, const double* uref, long uref_sb, double* u0, double* X, double* U,
-                     int* status, int nthreads) {
+                     long xref_sb, const double* uref, long uref_sb, const double* wind, long wind_sb,
+                     double* u0, double* X, double* U, int* status, int nthreads) {
   int bad = 0;
   const size_t wsz = (size_t)(N + 1) * NX + (size_t)N * NX * NZ + (size_t)N * NU * NX + (size_t)N * NU;
 #pragma omp parallel num_threads(nthreads) reduction(+ : bad)
@@ -228,7 +419,7 @@ int mpc_oracle_solve(int B, int N, const oracle_params* P, const double* x0, con
 #pragma omp for schedule(static)
     for (int b = 0; b < B; ++b) {
       int st = solve_one(N, P, x0 + (size_t)b * NX, xref + (size_t)b * xref_sb, uref + (size_t)b * uref_sb,
-                         u0 + (size_t)b * NU, X ? X + (size_t)b * (N + 1) * NX : NULL,
+                         wind ? wind + (size_t)b * wind_sb : NULL, u0 + (size_t)b * NU, X ? X + (size_t)b * (N + 1) * NX : NULL,
                          U ? U + (size_t)b * N * NU : NULL, work);
       if (status) status[b] = st;
       bad += st != 0;

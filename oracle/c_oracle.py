@@ -53,10 +53,9 @@ def _params(spec: OcpSpec) -> _Params:
     return p
 
 
-def solve(x0, xref, uref, spec: OcpSpec, nthreads: int = 1, want_traj: bool = True):
-    """Unconstrained rollout-mode SQP_RTI step (same algorithm as oracle.ocp.mpc_solve)."""
-    if spec.boxed:
-        raise NotImplementedError('the C oracle restates the unconstrained path only')
+def solve(x0, xref, uref, spec: OcpSpec, nthreads: int = 1, want_traj: bool = True, wind=None):
+    """Rollout-mode SQP_RTI step (same algorithm as oracle.ocp.mpc_solve): unconstrained, or with
+    the input box by the primal-dual active set of oracle.ocp.pdas_solve (then ``iters`` too)."""
     lib = load()
     x0 = np.ascontiguousarray(x0, dtype=np.float64)
     B, N = x0.shape[0], spec.N
@@ -71,7 +70,21 @@ def solve(x0, xref, uref, spec: OcpSpec, nthreads: int = 1, want_traj: bool = Tr
     P = _params(spec)
     dp = ctypes.POINTER(ctypes.c_double)
     ptr = lambda a: a.ctypes.data_as(dp) if a is not None else None  # noqa: E731
+    ip = ctypes.POINTER(ctypes.c_int)
+    if spec.boxed:
+        lb = np.ascontiguousarray(np.broadcast_to(np.asarray(spec.lbu, dtype=np.float64), (4,)))
+        ub = np.ascontiguousarray(np.broadcast_to(np.asarray(spec.ubu, dtype=np.float64), (4,)))
+        it = np.empty(B, dtype=np.int32)
+        lib.mpc_oracle_solve_box(ctypes.c_int(B), ctypes.c_int(N), ctypes.byref(P), ptr(lb), ptr(ub),
+                                 ctypes.c_int(spec.max_as_iter), ptr(x0), ptr(xr), ctypes.c_long(xr_sb), ptr(ur),
+                                 ctypes.c_long(ur_sb), ptr(u0), ptr(X), ptr(U), st.ctypes.data_as(ip),
+                                 it.ctypes.data_as(ip), ctypes.c_int(nthreads))
+        return dict(u0=u0, X=X, U=U, status=st, iters=it)
+    if wind is not None and spec.boxed:
+        raise NotImplementedError('wind with the input box')
+    wd = None if wind is None else np.ascontiguousarray(np.broadcast_to(wind, (B, 3)), dtype=np.float64)
     lib.mpc_oracle_solve(ctypes.c_int(B), ctypes.c_int(N), ctypes.byref(P), ptr(x0), ptr(xr),
-                         ctypes.c_long(xr_sb), ptr(ur), ctypes.c_long(ur_sb), ptr(u0), ptr(X), ptr(U),
+                         ctypes.c_long(xr_sb), ptr(ur), ctypes.c_long(ur_sb), ptr(wd), ctypes.c_long(3),
+                         ptr(u0), ptr(X), ptr(U),
                          st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.c_int(nthreads))
     return dict(u0=u0, X=X, U=U, status=st)
