@@ -132,7 +132,9 @@ template <class T> __device__ __forceinline__ Arr<T> arr(T* base, int rec, int64
   return Arr<T>{base ? base + ((c >> 2) * rec) * SS + (c & (SS - 1)) : nullptr, nq * rec * SS};
 }
 // row-major export (rec2): element e of the record at p0 + k * stride + e
-template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int64_t nq, int64_t c) {
+template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int64_t nq, int64_t c, int N, int imaj) {
+  // (mpcb_split.h rec2: instance-major or stage-major)
+  if (imaj) return Arr<T>{base ? base + c * N * (int64_t)rec : nullptr, rec};
   return Arr<T>{base ? base + ((c >> 2) * SS + (c & (SS - 1))) * rec : nullptr, nq * SS * rec};
 }
 
@@ -173,9 +175,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
   const int64_t nq = (nb + SS - 1) / SS;
   const Arr<T> XU = arr(a.XU, XU_REC, nq, c), GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
-  const Arr<T> AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c), ABT = arr2(a.ABT, ABT2_REC, nq, c);
-  const Arr<T> GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c), KR = arr2(a.KR, KR2_REC, nq, c);
-  const Arr<T> PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c);
+  const Arr<T> AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c, N, a.imajor), ABT = arr2(a.ABT, ABT2_REC, nq, c, N, a.imajor);
+  const Arr<T> GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c, N, a.imajor), KR = arr2(a.KR, KR2_REC, nq, c, N, a.imajor);
+  const Arr<T> PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c, N, a.imajor);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
   // the stage cost of direction j, when a backward stage needs it

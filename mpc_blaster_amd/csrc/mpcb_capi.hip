@@ -403,6 +403,8 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // row-major exports for the active-set kernel and the 16-lane forward pass; the optional
       // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
       a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
+      a.imajor = h->cfg.box_u ? 0 : 1;
+      if (const char* e = getenv("MPCB_RM_IMAJOR")) a.imajor = atoi(e) != 0;
       a.AB = (h->cfg.box_u || h->small) ? ab : nullptr;
       a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;

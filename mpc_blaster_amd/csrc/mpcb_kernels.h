@@ -109,6 +109,9 @@ struct SplitArgs {
   int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
   int rm;            // 1: P2 writes the row-major exports (AB2, ABT2, GH2, KR2 in a.AB/a.ABT/a.GH/a.KR)
+  int imajor;        // row-major exports instance-major (an instance's N records contiguous: the
+                     // unconstrained fp64 forward, measured -2 % per c2 step) or stage-major (the box
+                     // path: P2's scattered export stores measured 10 % slower instance-major at c4)
 };
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,

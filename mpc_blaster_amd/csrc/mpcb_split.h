@@ -122,11 +122,13 @@ __device__ __forceinline__ T* soa(T* base, int k, int rec, int64_t nb, int64_t c
   return base + (((int64_t)k * nq + (c >> 2)) * rec) * SS + (c & (SS - 1));
 }
 
-// Row-major export records (mpcb_kernels.h AB2_REC ...): record of chunk instance c at stage k.
+// Row-major export records (mpcb_kernels.h AB2_REC ...): record of chunk instance c at stage k,
+// instance-major (imaj: an instance's N records contiguous, so a 16-lane group walks one region
+// stage by stage) or stage-major (stage k of every instance, then stage k + 1): SplitArgs::imajor.
 template <class T>
-__device__ __forceinline__ T* rec2(T* base, int k, int rec, int64_t nb, int64_t c) {
+__device__ __forceinline__ T* rec2(T* base, int k, int rec, int64_t nb, int64_t c, int N, int imaj) {
   const int64_t nq = (nb + SS - 1) / SS;
-  return base + (((int64_t)k * nq + (c >> 2)) * SS + (c & (SS - 1))) * rec;
+  return base + (imaj ? c * N + k : ((int64_t)k * nq + (c >> 2)) * SS + (c & (SS - 1))) * (int64_t)rec;
 }
 
 // n contiguous elements through 16-B vector accesses (p 16-B aligned, n * sizeof(T) % 16 == 0)

@@ -440,9 +440,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       STAMP(1);
       const int tv = var_index(j);   // exported: the state-dependent columns only
       if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
-        if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c) + tv * NX, col);
+        if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c, N, a.imajor) + tv * NX, col);
         if (a.ABT && valid) {
-          T* abt = rec2(a.ABT, k, ABT2_REC, nb, c);
+          T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor);
           if (tv >= 0) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) abt[i * 12 + tv] = col[i];
@@ -536,7 +536,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NZ; ++i) row[i] = G[i];
       row[NZ] = hj;
       row[17] = row[18] = row[19] = T(0);
-      stv<T, 20>(rec2(a.GH, k, GH2_REC, nb, c) + ju * 20, row);
+      stv<T, 20>(rec2(a.GH, k, GH2_REC, nb, c, N, a.imajor) + ju * 20, row);
     }
 #pragma unroll
     for (int m = 0; m < NU; ++m) L.Hu[j * HS + m] = G[NX + m];
@@ -585,7 +585,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(6);
     kff0 = sel<NU>(kff, ju);
     if (valid && a.rm) {   // KR2: K[m][j] at 16 m + j, k_m at 16 m + 12
-      T* kr = rec2(a.KR, k, KR2_REC, nb, c);
+      T* kr = rec2(a.KR, k, KR2_REC, nb, c, N, a.imajor);
       if (j < NX) {
 #pragma unroll
         for (int m = 0; m < NU; ++m) kr[m * 16 + j] = Kj[m];
