@@ -205,6 +205,9 @@ struct Ctx {
   const T* sR;        // s * R (6 x 6), LDS
   int t, s, z, m;     // lane in the row, owned state, z column, input index (input lanes; else 0)
   bool in, valid;
+  int ks;             // 1; 0 once the group is parked (finished, outputs written): every stage-indexed
+                      // workspace access then goes to stage 0, so a finished group riding along with
+                      // its wave's others moves no HBM traffic
 };
 
 // state-box row (k, i): dx-coordinate bounds, the iterate and its slacks / multipliers
@@ -237,6 +240,7 @@ struct Pre {
 
 template <class T>
 __device__ __forceinline__ void prefetch(const Ctx<T>& r, int k, Pre<T>& p) {
+  k *= r.ks;
   const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
 #pragma unroll
   for (int i = 0; i < NX17; ++i) p.ab[i] = ABk[r.z * NX17 + i];
@@ -260,8 +264,9 @@ struct Cur {
   T ddxs, ddx8;                         // the last Newton step of dx_k[s], dx_k[8] (pending)
   T ixs[4], ix8[4];                     // state rows (s_l, s_u, lambda_l, lambda_u) of s and 8
 };
-template <class T>
+template <class T, bool SBX = true>
 __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
+  k *= r.ks;
   const int64_t kx = (int64_t)k * NX17;
   p.dxs = r.w.DX[kx + r.s];
   p.dx8 = r.w.DX[kx + OM];
@@ -271,11 +276,13 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
   p.du = ip[r.m];
   p.ll = ip[6 + r.m];
   p.lu = ip[12 + r.m];
-  const T* ix = r.w.IX + (int64_t)k * 4 * NX17;
+  if constexpr (SBX) {   // the state rows (SBX: the kernel can have a state box)
+    const T* ix = r.w.IX + (int64_t)k * 4 * NX17;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    p.ixs[e] = ix[e * NX17 + r.s];
-    p.ix8[e] = ix[e * NX17 + OM];
+    for (int e = 0; e < 4; ++e) {
+      p.ixs[e] = ix[e * NX17 + r.s];
+      p.ix8[e] = ix[e * NX17 + OM];
+    }
   }
 }
 
@@ -287,12 +294,14 @@ __device__ __forceinline__ void load_cur(const Ctx<T>& r, int k, Cur<T>& p) {
 // row takes the augmented-Lagrangian terms of its active side instead of the barrier: D = rho and
 // d = nu + rho (y - b) on an active row (side != 0), nothing on an inactive one.  The rows then hold
 // (nu, side) where the multipliers (lambda_l, lambda_u) were: IP[6 + m], IP[12 + m] and IX rows 2, 3.
-template <class T, bool MEH = false, bool POLC = false>
+// SBX: the kernel instantiation can carry state rows (the fp64 state-box kernel); the others
+// (the input box alone: Mehrotra in fp64, fp32) compile the state-row code and its registers out.
+template <class T, bool MEH = false, bool POLC = false, bool SBX = true>
 __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0), bool pol = false) {
   const FullArgs<T>& a = r.a;
   const bool ipm = a.box != 0;
   const bool gaps = !ipm && a.mode == MPCB_MODE_ITERATE;
-  const bool sbox = ipm && a.sbox != 0;
+  const bool sbox = SBX && ipm && a.sbox != 0;
   Lds<T>& L = r.L;
   const int t = r.t, s = r.s, N = a.N;
   const bool in = r.in;
@@ -302,10 +311,11 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
   // terminal cost: P_N = QN, p_N = QN (x_N - xref_N)
   T Pc[NX17], P88, pj, p8;
   {
-    T xs = r.w.XB[(int64_t)N * NX17 + s], x8 = r.w.XB[(int64_t)N * NX17 + OM];
+    const int Nq = N * r.ks;   // (a parked group: stage 0)
+    T xs = r.w.XB[(int64_t)Nq * NX17 + s], x8 = r.w.XB[(int64_t)Nq * NX17 + OM];
     if (ipm) {
-      T* dxn = r.w.DX + (int64_t)N * NX17;
-      const T* ddn = r.w.DDX + (int64_t)N * NX17;
+      T* dxn = r.w.DX + (int64_t)Nq * NX17;
+      const T* ddn = r.w.DDX + (int64_t)Nq * NX17;
       // (a select, not a product with apend = 0: DDX is not yet written before the first step)
       const T ys = (apend != T(0)) ? dxn[s] + apend * ddn[s] : dxn[s];
       const T y8 = (apend != T(0)) ? dxn[OM] + apend * ddn[OM] : dxn[OM];
@@ -314,8 +324,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       xs += ys;
       x8 += y8;
     }
-    L.V[s] = xs - r.xr[(int64_t)N * NX17 + s];
-    L.V[OM] = x8 - r.xr[(int64_t)N * NX17 + OM];
+    L.V[s] = xs - r.xr[(int64_t)Nq * NX17 + s];
+    L.V[OM] = x8 - r.xr[(int64_t)Nq * NX17 + OM];
     wave_lds_sync();
     pj = T(0);
     p8 = T(0);
@@ -329,7 +339,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
     P88 = W.QN[OM * NX17 + OM];
     wave_lds_sync();
     if constexpr (MEH) {   // p_N for the corrector's vector pass
-      T* gv = r.wm.GV + (int64_t)N * 24;
+      T* gv = r.wm.GV + (int64_t)Nq * 24;
       gv[s] = pj;
       gv[OM] = p8;
     }
@@ -344,12 +354,13 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
   for (int k = N - 1; k >= 0; --k) {
     const Pre<T> cu = nx;
     prefetch(r, k > 0 ? k - 1 : 0, nx);   // (unconditional: no branch join on the loads)
+    const int kq = k * r.ks;   // workspace stage (a parked group: 0)
     Cur<T> ic;
-    if (ipm) load_cur(r, k, ic);
+    if (ipm) load_cur<T, SBX>(r, k, ic);
     // pt = p + P gap (iterate mode)
     T pt = pj, pt8 = p8;
     if (gaps) {
-      const T* gk = r.w.GP + (int64_t)k * NX17;
+      const T* gk = r.w.GP + (int64_t)kq * NX17;
       T prow = Pc[OM] * gk[s];   // P[8, s] gap[s]: summed over the row below
 #pragma unroll
       for (int i = 0; i < NX17; ++i) pt += Pc[i] * gk[i];
@@ -382,8 +393,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
     if (ipm) {   // the pending step of this stage's iterate (unconditional stores)
       ic.dxs = (apend != T(0)) ? ic.dxs + apend * ic.ddxs : ic.dxs;
       ic.dx8 = (apend != T(0)) ? ic.dx8 + apend * ic.ddx8 : ic.dx8;
-      r.w.DX[(int64_t)k * NX17 + s] = ic.dxs;
-      r.w.DX[(int64_t)k * NX17 + OM] = ic.dx8;
+      r.w.DX[(int64_t)kq * NX17 + s] = ic.dxs;
+      r.w.DX[(int64_t)kq * NX17 + OM] = ic.dx8;
     }
     // cost residual (ybar [+ iterate] - yref) into LDS (general Q, R)
     L.V[s] = (ipm ? cu.xs + ic.dxs : cu.xs) - cu.xrs;
@@ -475,7 +486,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       }
       if constexpr (MEH) {   // (no state rows in the Mehrotra kernel: the gradients are complete)
         h8 = h8 + gr8;
-        T* gv = r.wm.GV + (int64_t)k * 24;
+        T* gv = r.wm.GV + (int64_t)kq * 24;
         gv[s] = gs;
         gv[OM] = gr8;
         gv[in ? NX17 + r.m : 23] = gu_own;
@@ -519,7 +530,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       for (int i = 0; i < NU17; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) pk[i * (i + 1) / 2 + j] = Lc[i * NU17 + j];
-      T* lc = r.wm.LC + (int64_t)k * WsM17<T>::LC_N;
+      T* lc = r.wm.LC + (int64_t)kq * WsM17<T>::LC_N;
       lc[t] = sel<16>(pk, t);
       lc[16 + t % 5] = sel<5>(pk + 16, t % 5);
     }
@@ -541,7 +552,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
     {   // KR: K row-major [6][17], then k[6].  Unconditional stores (a padding group owns its slot):
         // the K column of state 8 and k are the same in every lane (each lane solved the same
         // 6x6 systems), so every lane writes them to a fixed or its own input's slot
-      T* kr = r.w.KR + (int64_t)k * KR_N;
+      T* kr = r.w.KR + (int64_t)kq * KR_N;
 #pragma unroll
       for (int i = 0; i < NU17; ++i) {
         kr[i * NX17 + s] = Ks[i];
@@ -621,6 +632,7 @@ struct PreC {
 
 template <class T>
 __device__ __forceinline__ void prefetch_c(const Ctx<T>& r, int k, PreC<T>& p) {
+  k *= r.ks;
   const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
 #pragma unroll
   for (int i = 0; i < NX17; ++i) p.ab[i] = ABk[r.z * NX17 + i];
@@ -650,7 +662,7 @@ template <class T>
 __device__ __forceinline__ void backward_corr(const Ctx<T>& r, T smu) {
   const int s = r.s, N = r.a.N;
   const bool in = r.in;
-  T pc = r.wm.GV[(int64_t)N * 24 + s], pc8 = r.wm.GV[(int64_t)N * 24 + OM];
+  T pc = r.wm.GV[(int64_t)N * r.ks * 24 + s], pc8 = r.wm.GV[(int64_t)N * r.ks * 24 + OM];
   PreC<T> nx;
   prefetch_c(r, N - 1, nx);
   for (int k = N - 1; k >= 0; --k) {
@@ -681,7 +693,7 @@ __device__ __forceinline__ void backward_corr(const Ctx<T>& r, T smu) {
 #pragma unroll
     for (int n = 0; n < NU17; ++n) nb[n] = -h6[n];
     chol_n_solve<T, NU17>(Lc, nb, kc);
-    r.w.KR[(int64_t)k * Ws17<T>::KR_N + NU17 * NX17 + r.m] = sel<NU17>(kc, r.m);
+    r.w.KR[(int64_t)k * r.ks * Ws17<T>::KR_N + NU17 * NX17 + r.m] = sel<NU17>(kc, r.m);
     T pn = hs, pn8 = h8;
     static_for<NU17>([&](auto n) {
       constexpr int n_ = decltype(n)::value;
@@ -724,6 +736,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   constexpr int FD = STEP ? MPCB_Q17_FD_STEP : MPCB_Q17_FD;
   struct Row { T kr[LN], k8, kf, du, ab[LN], ab8o, c8s, c88, gs, g8, xbs, xb8, ubm; };
   auto load = [&](int k, Row& o) {
+    k *= r.ks;
     const T* ABk = r.w.AB + (int64_t)k * NZ17 * NX17;
     if constexpr (GAIN) {
       const T* Kk = r.w.KR + (int64_t)k * KR_N;
@@ -766,8 +779,9 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     // input lanes' du or (every other lane, the same value) the state-8 entry
     if constexpr (STEP || !OUT) {
       T* base = STEP ? ddx : r.w.DX;
-      base[(int64_t)k * NX17 + s] = dxs;
-      T* p2 = (STEP && in) ? ddu + (int64_t)k * NU17 + r.m : base + (int64_t)k * NX17 + OM;
+      const int kq = k * r.ks;
+      base[(int64_t)kq * NX17 + s] = dxs;
+      T* p2 = (STEP && in) ? ddu + (int64_t)kq * NU17 + r.m : base + (int64_t)kq * NX17 + OM;
       *p2 = (STEP && in) ? du : dx8;
     }
     if constexpr (OUT) {
@@ -811,8 +825,8 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
   QSTAMP_DONE("fwd");
   if constexpr (STEP || !OUT) {
     T* base = STEP ? ddx : r.w.DX;
-    base[(int64_t)N * NX17 + s] = dxs;
-    base[(int64_t)N * NX17 + OM] = dx8;
+    base[(int64_t)N * r.ks * NX17 + s] = dxs;
+    base[(int64_t)N * r.ks * NX17 + OM] = dx8;
   }
   if constexpr (OUT) {
     if (write && a.X) {
@@ -853,8 +867,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   for (int e = lane; e < NX17 * NX17; e += 64) sQ[e] = a.s * W.Q[e];
   for (int e = lane; e < NU17 * NU17; e += 64) sR[e] = a.s * W.R[e];
   __syncthreads();
-  const Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), WsM17<T>(Ws17<T>(a.ws + c * full17_elems(N), N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
-                 lds_all[q], sQ, sR, t, s, zcol(t), m, in, valid};
+  Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), WsM17<T>(Ws17<T>(a.ws + c * full17_elems(N), N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
+           lds_all[q], sQ, sR, t, s, zcol(t), m, in, valid, 1};
   Lds<T>& L = r.L;
   const T* x0 = a.x0 + b * a.x0_sb;
   const T dx0s = iterate ? x0[s] - r.w.XB[s] : T(0);
@@ -862,7 +876,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   int32_t st = MPCB_STATUS_OK;
   bool fin;
   if constexpr (!BOX) {
-    if (!backward<T>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
+    if (!backward<T, false, false, false>(r, T(0))) st = MPCB_STATUS_QP_FAIL;
     __syncthreads();   // K and k are read back across lanes
     fin = forward<T, true, false, true>(r, dx0s, dx08, valid);
   } else {
@@ -881,7 +895,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     __syncthreads();
     forward<T, false, false, false>(r, dx0s, dx08, false);   // DX of the starting point
     __syncthreads();
-    const bool sbox = !MEH && a.sbox != 0;
+    // (a state box exists only with fp64 and without Mehrotra: launch_riccati17q, mpcb_create)
+    constexpr bool SBX = !MEH && sizeof(T) == 8;
+    const bool sbox = SBX && a.sbox != 0;
     // state rows: s = max(distance to the bound, theta w), lambda = 1
     auto srow_init = [&](int k, int i) {
       const T xb = r.w.XB[(int64_t)k * NX17 + i], y = r.w.DX[(int64_t)k * NX17 + i];
@@ -934,6 +950,38 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
     T mu = T(0), res = T(0);       // duality measure, state-row residual (of the current iterate)
     T part_n = T(0), res_n = T(0); // their partial sums over the lane's rows after an update
     T apend = T(0);                // the last step length, not yet applied to DX
+    // outputs of a finished group: X = xbar + dx, U = ubar + du of its final iterate (with the last
+    // step when it is still pending, + the polish's Delta); written when the group finishes, after
+    // which it is parked (Ctx::ks)
+    bool parked = false;
+    auto emit = [&]() {
+      fin = true;
+      for (int k = 0; k <= N; ++k) {   // (with the last step, when it is still pending)
+        T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
+        if (apend != T(0)) {
+          xs = xs + apend * r.w.DDX[(int64_t)k * NX17 + s];
+          x8 = x8 + apend * r.w.DDX[(int64_t)k * NX17 + OM];
+        }
+        if (POLC && pst == 2) {
+          xs = xs + r.w.DDX[(int64_t)k * NX17 + s];
+          x8 = x8 + r.w.DDX[(int64_t)k * NX17 + OM];
+        }
+        if (valid && a.X) {
+          T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
+          xo[s] = r.w.XB[(int64_t)k * NX17 + s] + xs;
+          if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + x8;
+        }
+        fin = fin && ((xs - xs) == T(0)) && ((x8 - x8) == T(0));
+        if (in && k < N) {
+          T duk = r.w.IP[(int64_t)k * 18 + m];
+          if (POLC && pst == 2) duk = duk + r.w.DDU[(int64_t)k * NU17 + m];
+          const T uo = r.w.UB[(int64_t)k * NU17 + m] + duk;
+          fin = fin && ((uo - uo) == T(0));
+          if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + m] = uo;
+          if (valid && k == 0) a.u0[b * NU17 + m] = uo;
+        }
+      }
+    };
     constexpr bool F64 = sizeof(T) == 8;
     const T ipm_tol = T(F64 ? IPM17_TOL : IPM17_TOL_F32), ipm_brk = T(F64 ? IPM17_BREAK : IPM17_BREAK_F32);
     const T ipm_res = T(F64 ? IPM17_RES : IPM17_RES_F32);
@@ -989,14 +1037,20 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         }
         __syncthreads();   // the rows of state 8 are read by every lane of the next backward
       }
-      if (__all((polish ? pst >= 2 : done) || !valid)) break;
+      const bool finished = polish ? pst >= 2 : done;
+      if (finished && !parked) {
+        emit();
+        parked = true;
+        r.ks = 0;
+      }
+      if (__all(finished || !valid)) break;
       QSTAMP(0);
       T smu;
       if constexpr (!MEH) {
       // centring follows the previous step: sigma = clip(1 - alpha, 0.05, 0.9)
       nit += (pst == 0 && !done) ? 1 : 0;
       smu = fmin(T(IPM17_SIGMA_MAX), fmax(T(IPM17_SIGMA_MIN), T(1) - prev_alpha)) * mu;
-      const bool ok_b = backward<T, false, POLC>(r, smu, apend, pst == 1 || pst == 2);
+      const bool ok_b = backward<T, false, POLC, SBX>(r, smu, apend, pst == 1 || pst == 2);
       apend = T(0);
       if (!ok_b && !done) {
         // a Newton system that lost positive definiteness near the solution: keep the current
@@ -1042,7 +1096,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
             }
           }
         };
-        if (in) {
+        if (in && pst == 1) {
           for (int k = 0; k < N; ++k) {
             const T ubk = r.w.UB[(int64_t)k * NU17 + m];
             T* ip = r.w.IP + (int64_t)k * 18;
@@ -1055,8 +1109,10 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
           prow(k, kind, r.w.DX[kx] + r.w.DDX[kx], W.lbx[i] - xb, W.ubx[i] - xb, ix + 2 * NX17, ix[3 * NX17]);
         };
-        for (int k = 1; k < N; ++k) srow(k, s, 1);
-        for (int k = 1 + t; k < N; k += LN) srow(k, OM, 2);
+        if (pst == 1) {
+          for (int k = 1; k < N; ++k) srow(k, s, 1);
+          for (int k = 1 + t; k < N; k += LN) srow(k, OM, 2);
+        }
         const T eq = row_max(eq_l), wmin = row_min(w_l), vmax = row_max(v_l);
         const bool rel = wmin < T(0);
         const bool add = !rel && vmax > T(POL17_FEAS);
@@ -1081,7 +1137,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       // predictor: targets 0 -> the affine direction into DAX / DAU (K, k, the factor of Huu and
       // the stage gradients stay in KR / LC / GV)
       nit += !done ? 1 : 0;
-      const bool ok_b = backward<T, true>(r, T(0), apend);
+      const bool ok_b = backward<T, true, false, false>(r, T(0), apend);
       apend = T(0);
       if (!ok_b && !done) {
         if (!(mu > ipm_brk)) {
@@ -1100,7 +1156,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       // and per input row w = 1/s_l - 1/s_u, c = Delta s_a Delta lambda_a / s_l - (upper) into DC
       // (the state entries zero: no state rows here)
       T aa = T(1), S0 = T(0), S1 = T(0), S2 = T(0);
-      if (in) {
+      if (in && !parked) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
@@ -1121,15 +1177,17 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           dc[24] = dsl * dll / sl - dsu * dlu / su;
         }
       }
-      for (int k = 0; k < N; ++k) {
-        T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
-        dc[s] = T(0);
-        dc[24 + s] = T(0);
-      }
-      for (int k = t; k < N; k += LN) {
-        T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
-        dc[OM] = T(0);
-        dc[24 + OM] = T(0);
+      if (!parked) {
+        for (int k = 0; k < N; ++k) {
+          T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
+          dc[s] = T(0);
+          dc[24 + s] = T(0);
+        }
+        for (int k = t; k < N; k += LN) {
+          T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N;
+          dc[OM] = T(0);
+          dc[24 + OM] = T(0);
+        }
       }
       aa = row_min(aa);
       const T mu_a = (row_sum(S0) + aa * row_sum(S1) + aa * aa * row_sum(S2)) / (T(2) * rows);
@@ -1150,7 +1208,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       T amax = T(1) / T(IPM17_TAU);
       bool dfin = true;   // a finite direction from strictly positive slacks
-      if (in) {
+      if (in && !parked) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
           const T ubk = r.w.UB[(int64_t)k * NU17 + m];
@@ -1171,7 +1229,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           if (dlu < T(0)) amax = fmin(amax, -lu / dlu);
         }
       }
-      if (sbox) {
+      if (sbox && !parked) {
         auto step_row = [&](int k, int i) {
           const SRow<T> sr(r, k, i);
           const T dy = r.w.DDX[(int64_t)k * NX17 + i];
@@ -1271,33 +1329,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       a.qp_stats[2 * b] = nit;
       a.qp_stats[2 * b + 1] = npass;
     }
-    // outputs: X = xbar + dx, U = ubar + du of the final iterate (+ the polish's Delta)
-    fin = true;
-    for (int k = 0; k <= N; ++k) {   // (with the last step, when it is still pending)
-      T xs = r.w.DX[(int64_t)k * NX17 + s], x8 = r.w.DX[(int64_t)k * NX17 + OM];
-      if (apend != T(0)) {
-        xs = xs + apend * r.w.DDX[(int64_t)k * NX17 + s];
-        x8 = x8 + apend * r.w.DDX[(int64_t)k * NX17 + OM];
-      }
-      if (POLC && pst == 2) {
-        xs = xs + r.w.DDX[(int64_t)k * NX17 + s];
-        x8 = x8 + r.w.DDX[(int64_t)k * NX17 + OM];
-      }
-      if (valid && a.X) {
-        T* xo = a.X + (b * (int64_t)(N + 1) + k) * NX17;
-        xo[s] = r.w.XB[(int64_t)k * NX17 + s] + xs;
-        if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + x8;
-      }
-      fin = fin && ((xs - xs) == T(0)) && ((x8 - x8) == T(0));
-      if (in && k < N) {
-        T duk = r.w.IP[(int64_t)k * 18 + m];
-        if (POLC && pst == 2) duk = duk + r.w.DDU[(int64_t)k * NU17 + m];
-        const T uo = r.w.UB[(int64_t)k * NU17 + m] + duk;
-        fin = fin && ((uo - uo) == T(0));
-        if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + m] = uo;
-        if (valid && k == 0) a.u0[b * NU17 + m] = uo;
-      }
-    }
+    if (!parked) emit();
   }
   // instance status: any lane's non-finite value marks the instance
   const int bad = row_or(fin ? 0 : 1);
