@@ -69,7 +69,7 @@ __device__ __forceinline__ void f17_tan(const T* __restrict__ x, const T* __rest
   trig(x, tsn, tcs);
   const T sf = tsn[0], cf = tcs[0], st = tsn[1], ct = tcs[1], sp = tsn[2], cp = tcs[2];
   const T s1 = tsn[3], c1 = tcs[3], s2 = tsn[4], c2 = tcs[4];
-  const T ict = T(1) / ct;
+  const T ict = recip(ct);
   const T tt = st * ict;
   const T wx = x[9], wy = x[10], wz = x[11];
   f[0] = x[6]; f[1] = x[7]; f[2] = x[8];

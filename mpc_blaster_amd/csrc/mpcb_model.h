@@ -65,6 +65,30 @@ __device__ __forceinline__ void sc(float a, float* s, float* c) {
   *c = ((q + 1) & 2) ? -c0 : c0;
 }
 
+// 1/x by the hardware reciprocal and two Newton steps (fp64: v_rcp_f64 + 4 FMAs, ~1 ulp; the
+// IEEE division sequence is ~11 instructions with its scale / fixup steps).  |x| is cos(theta) of a
+// flying attitude here, far from 0, denormals and infinity.  MPCB_IEEE_DIV=1 restores the division.
+#ifndef MPCB_IEEE_DIV
+#define MPCB_IEEE_DIV 0
+#endif
+__device__ __forceinline__ double recip(double x) {
+#if MPCB_IEEE_DIV
+  return 1.0 / x;
+#else
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+#endif
+}
+__device__ __forceinline__ float recip(float x) {
+#if MPCB_IEEE_DIV
+  return 1.0f / x;
+#else
+  const float r = __builtin_amdgcn_rcpf(x);
+  return fmaf(fmaf(-x, r, 1.0f), r, r);
+#endif
+}
+
 // f and (optionally) its tangent.  wind may be nullptr-equivalent (w0=w1=w2=0).
 template <class T, bool TAN>
 __device__ __forceinline__ void f_tan(const T* __restrict__ x, const T* __restrict__ dx,
@@ -75,7 +99,7 @@ __device__ __forceinline__ void f_tan(const T* __restrict__ x, const T* __restri
   sc(x[3], &sf, &cf);
   sc(x[4], &st, &ct);
   sc(x[5], &sp, &cp);
-  const T ict = T(1) / ct;
+  const T ict = recip(ct);
   const T tt = st * ict;
   const T wx = x[9], wy = x[10], wz = x[11];
   // ---- p_dot = v
@@ -218,7 +242,7 @@ __device__ __forceinline__ void f_nom_lin(const T* __restrict__ x, const T* __re
                                           T* __restrict__ c, const Trig& trig = Trig()) {
   T sf, cf, st, ct, sp, cp;
   trig(x, sf, cf, st, ct, sp, cp);
-  const T ict = T(1) / ct;
+  const T ict = recip(ct);
   const T tt = st * ict;
   const T wx = x[9], wy = x[10], wz = x[11];
   f[0] = x[6]; f[1] = x[7]; f[2] = x[8];
