@@ -258,6 +258,17 @@ def dispatches_per_phase(B: int) -> int:
     return -(-int(B) // chunk)
 
 
+def kernel_bytes(w, r, phase):
+    """Algorithmic HBM bytes of the active-set kernel (c4, the only phase whose binding resource
+    is memory): per forward stage the variable columns of [A|B] (12 x 10), K and k (4 x 13) and
+    (xbar, ubar) (16); per recomputed backward stage the [A|B] columns (120), the stage Hessian
+    rows it exports (4 x 17), K and k (52) and the value-function snapshot for restarts (12 x 13):
+    188 and 396 elements, counted from the kernel's own statistics (mpcb_qp_stats)."""
+    esz = 8 if w['dtype'] == 'f64' else 4
+    q = r['qp']
+    return esz * (188 * w['N'] * q['fwd_passes'] + 396 * q['bwd_stages'])
+
+
 def pmc_kernel(workload: str, kernel: str):
     """Counter-derived figures of one kernel from the committed PMC summary (tools/pmc_summary.py)."""
     p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
@@ -299,6 +310,7 @@ def summarize(w, r, world, steps):
     tr = tr * disp if tr else None
     roof = {'bound': 'valu', 'achieved': achieved_tf, 'peak': peak, 'unit': 'TFLOP/s',
             'frac': achieved_tf / peak, 'traffic': tr,
+            'valu_frac': achieved_tf / peak,
             'kernel': names[dom], 'kernel_ms': ph[dom], 'dispatches_per_phase': disp,
             'flop_per_phase': flop, 'executed_flop_per_phase': ex,
             'executed_frac': (ex / (ph[dom] * 1e-3) / 1e12 / peak) if ex else None,
@@ -317,13 +329,23 @@ def summarize(w, r, world, steps):
                      'on its launch stream); achieved = its dense algorithmic flops (bench.py '
                      'phase_kernels docstring) / that time. executed_frac = counter-executed flops '
                      '(64 x SQ_INSTS_VALU_FLOPS_FP32/FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F32, '
-                     'profiles/pmc_<workload>.json) over the same time. traffic = HBM bytes per '
+                     'profiles/pmc_<workload>.json) over the same time (c4: the active-set kernel is '
+                     'memory-bound, so bound = hbm, achieved = its algorithmic bytes, bench.py '
+                     'kernel_bytes, over its time; valu_frac keeps the flop view). traffic = HBM bytes per '
                      'phase of that kernel (per-dispatch PMC x dispatches_per_phase), '
                      '(2 x FETCH_SIZE + WRITE_SIZE) from the same PMC run '
                      '(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md). solve_* = every kernel '
                      'of the solve over the whole solve time.')}
     if r.get('qp'):
         roof['active_set'] = r['qp']
+    if w['box'] and dom == 'forward':
+        # the active-set kernel re-streams its exported rows every pass (PMC: 2.9 TB/s, 47 % of
+        # the wave time waiting): its binding resource is HBM, so that is the roofline it reports
+        byt = kernel_bytes(w, r, dom)
+        gbs = byt / (ph[dom] * 1e-3) / 1e9
+        roof.update(bound='hbm', achieved=gbs, peak=HBM_PEAK_GBS, unit='GB/s', frac=gbs / HBM_PEAK_GBS,
+                    bytes_per_phase=byt,
+                    traffic_frac=(tr / (ph[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS) if tr else None)
     return value, roof
 
 

@@ -853,9 +853,13 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   const int t = lane % LN;
   const int64_t c_raw = (int64_t)blockIdx.x * GR + q;
   const bool valid = c_raw < a.nb;
-  // a ragged last wave's extra groups run on private padding slots of the workspace (mpcb_create
-  // sizes it to whole wavefronts), so every workspace store is unconditional; their inputs and
-  // outputs are the last instance's
+  // A ragged last wave's extra groups (!valid) run on private padding slots of the workspace
+  // (mpcb_create sizes it to whole wavefronts), so every workspace store is unconditional.  Those
+  // slots are never filled (nominal17q / lin17ws write valid instances only): a padding group
+  // iterates on garbage, which is harmless because (1) every reduction and exchange is row-local
+  // (DPP row broadcasts, the group's own LDS block), so nothing flows into a valid group, (2) its
+  // outputs are never written (valid guards) and (3) the loop exit ignores it (__all(... || !valid)).
+  // Its x0 / xref / uref reads use the last instance's (b is clamped).
   const int64_t c = c_raw;
   const int64_t b = a.b0 + (valid ? c : a.nb - 1);
   const int N = a.N;

@@ -120,9 +120,37 @@ def main():
     if os.path.exists(pj) and args.dtype == 'f64' and B == 4096 and N == 60:
         e = json.load(open(pj)).get('per_kernel', {}).get('mpcb::' + kname, {}).get('executed_flops_per_launch')
         ex = e / (ph['riccati'] * 1e-3) / 1e12 / peak if e else None
-    roof = {'bound': 'valu', 'kernel': kname, 'flop_per_stage': fl, 'flop_per_launch': flop,
-            'achieved': ach, 'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak, 'executed_frac': ex,
-            'kernel_ms': ph['riccati']}
+    # HBM view.  Algorithmic bytes per instance-stage of one interior-point iteration (fp64): the
+    # backward reads the 16 dense [A|B] columns and the 5 nonzeros of the shear column (277) and
+    # writes K, k (108); the Newton-step forward reads the same rows (277) and K, k (108): 770
+    # doubles; Mehrotra adds the corrector's vector pass (277 + 108 + the factor 21, gradients 24,
+    # row terms 48, k 6) and its forward (385): 1639 doubles.  A polish pass is a plain iteration.
+    # The unconstrained pass: one backward + forward (770).  traffic = the PMC's HBM bytes per
+    # launch (profiles/pmc_full17*.json, (2 FETCH_SIZE + WRITE_SIZE) KiB) at the profiled size.
+    esz = 8 if args.dtype == 'f64' else 4
+    it_b = (770 + (869 if meh else 0)) * esz
+    if box:
+        byt = (it_b * qp['iters_total'] + 770 * esz * qp['polish_total']) * N
+    else:
+        byt = 770 * esz * N * B
+    tr = None
+    if os.path.exists(pj) and args.dtype == 'f64' and B == 4096 and N == 60:
+        tr = json.load(open(pj)).get('per_kernel', {}).get('mpcb::' + kname, {}).get('hbm_bytes_per_launch')
+    hbm = {'achieved': byt / (ph['riccati'] * 1e-3) / 1e9, 'peak': 8000.0, 'unit': 'GB/s',
+           'bytes_per_launch': byt, 'bytes_per_iteration_stage': it_b, 'traffic': tr,
+           'traffic_GBs': tr / (ph['riccati'] * 1e-3) / 1e9 if tr else None}
+    hbm['frac'] = hbm['achieved'] / hbm['peak']
+    hbm['traffic_frac'] = hbm['traffic_GBs'] / hbm['peak'] if tr else None
+    # the boxed kernels stream their [A|B] and gains every iteration: their binding resource is
+    # memory (B = 1024 -> 4096 at the same iteration count: 10.1 -> 17.1 ms, profiles/r03), the
+    # unconstrained pass is issue-bound (VALU)
+    roof = {'bound': 'hbm' if box else 'valu', 'kernel': kname, 'kernel_ms': ph['riccati'],
+            'valu': {'achieved': ach, 'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak,
+                     'executed_frac': ex, 'flop_per_stage': fl, 'flop_per_launch': flop},
+            'hbm': hbm}
+    main = hbm if box else roof['valu']
+    roof.update(achieved=main['achieved'], peak=main['peak'], unit=main['unit'], frac=main['frac'],
+                traffic=tr, executed_frac=ex)
     if qp:
         roof.update(interior_point=qp, flop_per_iteration_stage=it_fl, flop_per_polish_stage=pol_fl)
     print(json.dumps({'metric': f'MPC solves/sec (full 17/6 model, N={N})', 'value': B * args.steps / el,
