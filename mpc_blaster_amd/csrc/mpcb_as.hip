@@ -238,12 +238,23 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) Pc[i] = qn[i];
         if (kc >= 0 && kc < N - 1 && stl) {   // restart: the value function stored at kc + 1
-          T ps[16];
-          ldv<T, 16>(PS.at(kc + 1) + jx * 16, ps);
+          // P[i][j] sits with lane i at slot (j - i) % 12 when that is <= 6, else with lane j at
+          // slot (i - j) % 12 (the packed PS2 record, mpcb_kernels.h)
+          // (unpacked through the group's LDS block: per-lane LDS offsets instead of 12 global
+          // addresses, which the compiler kept live into a spill)
+          T ps[PS2_W];
+          ldv<T, PS2_W>(PS.at(kc + 1) + jx * PS2_W, ps);
 #pragma unroll
-          for (int i = 0; i < NX; ++i) Pc[i] = ps[i];
-          pj = ps[NX];
+          for (int d = 0; d < PS2_W; ++d) PX[jx * PS2_W + d] = ps[d];
+          wave_lds_sync();
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            const int dd = (jx - i + NX) % NX;
+            Pc[i] = PX[dd <= 6 ? i * PS2_W + dd : jx * PS2_W + (NX - dd)];
+          }
+          pj = ps[7];
         }
+        wave_lds_sync();   // the stages' PX writes follow the reads
       }
       bool qp_ok = true;
       // stage data one stage ahead: column j of [A|B], own (ybar - yref) and ybar components,
@@ -314,7 +325,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           for (int i = 0; i < NZ; ++i) G[i] += swc[i];
         }
         ASTAMP(1);
-        if (act && valid && !stl) {   // unmasked input rows: the forward's multipliers
+        // unmasked input row of a component fixed at this stage: the forward's multiplier.  (Where
+        // the component is free the forward never reads the row, and a stage whose fixed set
+        // changes is recomputed -- and its row written -- before the next forward pass.)
+        if (act && valid && !stl && (((lowm | upm) >> k) & 1ull)) {
           T gr[20];
 #pragma unroll
           for (int i = 0; i < NZ; ++i) gr[i] = G[i];
@@ -384,13 +398,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         for (int i = 0; i < NX; ++i) Pn[i] = G[i];
 #pragma unroll
         for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
-        if (act && valid) {   // KR2: K[m][j] at 16 m + j, k_m at 16 m + 12
+        if (act && valid) {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
           T* kr = KR.at(k);
           if (stl) {
 #pragma unroll
-            for (int m = 0; m < NU; ++m) kr[m * 16 + j] = Kj[m];
+            for (int m = 0; m < NU; ++m) kr[m * KR2_W + j] = Kj[m];
           } else {
-            kr[ju * 16 + 12] = sel<NU>(kff, ju);
+            kr[ju * KR2_W + 12] = sel<NU>(kff, ju);
           }
         }
         ASTAMP(2);
@@ -410,15 +424,19 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           }
           pj = csel(ma, csel(mst, pn, T(0)), pj);
         }
-        wave_lds_sync();
-        if (act && valid && stl && k > 0) {   // snapshot P_k, p_k for a later restart
-          T ps[16];
+        // packed snapshot of P_k, p_k for a later restart: slot d of lane j is P[j][(j + d) % 12],
+        // the entry lane max(j, o) published above
+        if (act && valid && stl && k > 0) {
+          T ps[PS2_W];
 #pragma unroll
-          for (int i = 0; i < NX; ++i) ps[i] = Pc[i];
-          ps[NX] = pj;
-          ps[13] = ps[14] = ps[15] = T(0);
-          stv<T, 16>(PS.at(k) + j * 16, ps);
+          for (int d = 0; d < 7; ++d) {
+            const int o = jx + d < NX ? jx + d : jx + d - NX;
+            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
+          }
+          ps[7] = pj;
+          stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);
         }
+        wave_lds_sync();
         ASTAMP(3);
       }
       if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
@@ -442,15 +460,16 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     // use: moving them on arrival would make the compiler wait for the loads right away.
     // (The Hessian rows, needed at few stages, come one stage ahead through a single slot.)
     constexpr int FD = BOX ? MPCB_AS_FDEPTH : MPCB_FWD_FDEPTH;
-    constexpr int FL = sizeof(T) == 8 ? 14 : 16;
-    T pv[FD][FL], pyb[FD], pg[20];
+    constexpr int FL = KR2_W;
+    T pv[FD][FL], pyb[FD], pgp[FD], pg[20];
     auto rload = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
       pyb[sl] = XU.at(k)[j * SS];
-      // one load for both kinds of lane, from a per-lane address: the 13 elements an input lane
-      // uses rounded up to 16-B vectors (14 in fp64, 16 in fp32); a state lane's 12-element
-      // ABT2 row is followed by the next row or record, or by the workspace padding
-      ldv<T, FL>(stl ? ABT.at(k) + jx * 12 : KR.at(k) + ju * 16, pv[sl]);
+      // one load for both kinds of lane, from a per-lane address: an input lane's KR2 row (13
+      // elements used), a state lane's 10-element ABT2 row followed by the next row or record,
+      // or by the workspace padding; 8-B vectors in fp32 (rows start 8-B aligned), 16-B in fp64
+      ldv<T, FL, sizeof(T) == 8 ? 16 : 8>(stl ? ABT.at(k) + jx * ABT2_W : KR.at(k) + ju * KR2_W, pv[sl]);
+      if (iterate) pgp[sl] = GP.at(k)[jx * SS];   // state lanes: gap_jx (input lanes: unused)
     };
     auto gload = [&](int k) {
       if (BOX && (((lowm | upm) >> k) & 1ull)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
@@ -477,7 +496,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         row[p] = csel(mst, crow[p], row[p]);
         row[6 + p] = csel(mst, crow[3 + p], row[6 + p]);
       }
-      const T r0 = csel(mst, iterate ? pv[sl][NVAR] : T(0), BOX ? csel(mfix, pg[NZ], T(0)) : T(0));
+      const T r0 = csel(mst, iterate ? pgp[sl] : T(0), BOX ? csel(mfix, pg[NZ], T(0)) : T(0));
       const T yb = pyb[sl];
       ASTAMP(4);
       // du = k + K dx (input lanes; dx_i broadcast from state lane i)

@@ -74,14 +74,19 @@ __host__ __device__ constexpr int var_index(int j) { return (j >= 3 && j < 6) ? 
 constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 // Row-major exports (SplitArgs::rm = 1: the input-box kernel mpcb_as.hip and the 16-lane forward
 // pass of small unconstrained chunks).  Per stage the 4 instances of a quad follow each other and
-// each instance's record is contiguous, so a lane's row (or column) is a run of 16-B-aligned
-// vectors (mpcb_split.h rec2()):
+// each instance's record is contiguous, so a lane's row (or column) is a run of aligned vectors
+// (mpcb_split.h rec2()); rows carry no padding beyond what the vector width needs:
 //   AB2  [10][12]  column var_col(t) of [A|B], 12 entries       (backward: lane var_col(t))
-//   ABT2 [12][12]  row i of [A|B] at the variable columns t < 10, slot 10 = gap_i (iterate)
-//   KR2  [4][16]   row m of K (12 entries), slot 12 = k_m
-//   GH2  [4][20]   row m of the stage Hessian's input rows (16 entries), slot 16 = h_u[m]
-//   PS2  [12][16]  column j of P_k (12 entries), slot 12 = p_k[j]
-constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * 12, KR2_REC = 4 * 16, GH2_REC = 4 * 20, PS2_REC = 12 * 16;
+//   ABT2 [12][10]  row i of [A|B] at the variable columns t < 10 (forward: state lane i; the
+//                  iterate-mode gap comes from GP)
+//   KR2  [4][14]   row m of K (12 entries), slot 12 = k_m
+//   GH2  [4][20]   row m of the stage Hessian's input rows (16 entries), slot 16 = h_u[m]; written
+//                  by the active-set kernel's masked backward, only where component m is fixed
+//   PS2  [12][8]   P_k packed by symmetry: lane j keeps P[j][(j + d) % 12], d = 0..6, and p_k[j]
+//                  in slot 7 (84 slots for its 78 distinct entries)
+constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
+constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, GH2_REC = 4 * 20,
+              PS2_REC = 12 * PS2_W;
 
 template <class T>
 struct SplitArgs {

@@ -131,10 +131,10 @@ __device__ __forceinline__ T* rec2(T* base, int k, int rec, int64_t nb, int64_t 
   return base + (imaj ? c * N + k : ((int64_t)k * nq + (c >> 2)) * SS + (c & (SS - 1))) * (int64_t)rec;
 }
 
-// n contiguous elements through 16-B vector accesses (p 16-B aligned, n * sizeof(T) % 16 == 0)
-template <class T, int n> __device__ __forceinline__ void ldv(const T* __restrict__ p, T* v) {
-  constexpr int W = 16 / sizeof(T);
-  static_assert((n % W) == 0, "ldv: whole 16-B vectors");
+// n contiguous elements through VB-byte vector accesses (p VB-byte aligned, n * sizeof(T) % VB == 0)
+template <class T, int n, int VB = 16> __device__ __forceinline__ void ldv(const T* __restrict__ p, T* v) {
+  constexpr int W = VB / sizeof(T);
+  static_assert(W >= 1 && (n % W) == 0, "ldv: whole vectors");
   typedef T V __attribute__((ext_vector_type(W)));
   const V* vp = reinterpret_cast<const V*>(p);
 #pragma unroll

@@ -441,13 +441,10 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       const int tv = var_index(j);   // exported: the state-dependent columns only
       if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
         if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c, N, a.imajor) + tv * NX, col);
-        if (a.ABT && valid) {
+        if (a.ABT && valid && tv >= 0) {
           T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor);
-          if (tv >= 0) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) abt[i * 12 + tv] = col[i];
-          }
-          if (iterate && j < NX) abt[j * 12 + NVAR] = cc[CCS_REC + j];   // gap_j
+          for (int i = 0; i < NX; ++i) abt[i * ABT2_W + tv] = col[i];
         }
       } else {
         if (EXPORT && a.AB && valid && tv >= 0) {
@@ -530,14 +527,8 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       G[i] += w;
       hj += w * L.v[i];
     }
-    if (EXPORT && a.GH && valid && j >= NX) {   // box path: always row-major (GH2)
-      T row[20];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) row[i] = G[i];
-      row[NZ] = hj;
-      row[17] = row[18] = row[19] = T(0);
-      stv<T, 20>(rec2(a.GH, k, GH2_REC, nb, c, N, a.imajor) + ju * 20, row);
-    }
+    // (box path: no Hessian rows here -- the active set is empty in this pass, and the first
+    // masked backward recomputes every stage and writes the rows its fixed components need)
 #pragma unroll
     for (int m = 0; m < NU; ++m) L.Hu[j * HS + m] = G[NX + m];
     wave_lds_sync();
@@ -584,13 +575,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     STAMP(6);
     kff0 = sel<NU>(kff, ju);
-    if (valid && a.rm) {   // KR2: K[m][j] at 16 m + j, k_m at 16 m + 12
+    if (valid && a.rm) {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
       T* kr = rec2(a.KR, k, KR2_REC, nb, c, N, a.imajor);
       if (j < NX) {
 #pragma unroll
-        for (int m = 0; m < NU; ++m) kr[m * 16 + j] = Kj[m];
+        for (int m = 0; m < NU; ++m) kr[m * KR2_W + j] = Kj[m];
       } else {
-        kr[ju * 16 + 12] = kff0;
+        kr[ju * KR2_W + 12] = kff0;
       }
     } else if (valid) {
       // K[m][j] at 4j + m (state lanes), kff[m] at 4*NX + m (input lanes): the first store is
