@@ -182,13 +182,15 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
   // the stage cost of direction j, when a backward stage needs it
   __shared__ T SW[NZ * NZ];
-  for (int e = lane; e < NZ * NZ; e += 64) {
-    const int r = e / NZ, cl = e % NZ;
-    const T wq = (r < NX && cl < NX) ? W.Q[r * NX + cl] : T(0);
-    const T wr = (r >= NX && cl >= NX) ? W.R[(r - NX) * NU + (cl - NX)] : T(0);
-    SW[e] = a.s * (wq + wr);
+  if constexpr (BOX) {   // (the backward pass's; the forward-only instantiation allocates no LDS)
+    for (int e = lane; e < NZ * NZ; e += 64) {
+      const int r = e / NZ, cl = e % NZ;
+      const T wq = (r < NX && cl < NX) ? W.Q[r * NX + cl] : T(0);
+      const T wr = (r >= NX && cl >= NX) ? W.R[(r - NX) * NU + (cl - NX)] : T(0);
+      SW[e] = a.s * (wq + wr);
+    }
+    wave_lds_sync();
   }
-  wave_lds_sync();
   // row i of [A|B] at the constant columns (state lanes): position e_p, velocity e_v + h e_p
   T crow[6];
 #pragma unroll
