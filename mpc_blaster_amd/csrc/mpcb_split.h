@@ -94,6 +94,19 @@ __device__ __forceinline__ void fmac16_diag(double (&acc)[16], double a, double 
       : "v"(a), "v"(b));
 }
 
+// acc[i] += bcast_i(a) * b for the 10 variable directions i = 3..5, 9..15 (mpcb_kernels.h var_col):
+// the rows of G = [A|B]^T Y whose [A|B] column depends on the linearisation point
+__device__ __forceinline__ void fmac10_var(double (&acc)[16], double a, double b) {
+  asm("s_nop 4\n\t"
+      MPCB_BC(0, 10, 11, "3") MPCB_BC(1, 10, 11, "4") MPCB_BC(2, 10, 11, "5")
+      MPCB_BC(3, 10, 11, "9") MPCB_BC(4, 10, 11, "10") MPCB_BC(5, 10, 11, "11")
+      MPCB_BC(6, 10, 11, "12") MPCB_BC(7, 10, 11, "13") MPCB_BC(8, 10, 11, "14")
+      MPCB_BC(9, 10, 11, "15")
+      : "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11]),
+        "+v"(acc[12]), "+v"(acc[13]), "+v"(acc[14]), "+v"(acc[15])
+      : "v"(a), "v"(b));
+}
+
 // acc[i] += bcast_i(a) * b  (i < 12)
 __device__ __forceinline__ void fmac12_diag(double (&acc)[12], double a, double b) {
   asm("s_nop 4\n\t"

@@ -53,6 +53,9 @@
 #define MPCB_P2_PCSEL 0
 #endif
 
+#ifndef MPCB_P2_GVAR   // fp64 P2: G's rows at the constant directions without broadcasts
+#define MPCB_P2_GVAR 1
+#endif
 #ifndef MPCB_P2_WAVES_F32
 #define MPCB_P2_WAVES_F32 2
 #endif
@@ -367,6 +370,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   const int64_t nb = a.nb;
   const T* xr = a.xref + b * a.xref_sb;
   const T* ur = a.uref + b * a.uref_sb;
+  const T hv = (a.h / T(6)) * T(6);   // the RK4 tangent's position entry of a velocity column
 
   // s * blkdiag(Q, R) in LDS: lane j reads column j (= row j), so the stage-cost terms are the
   // same instruction stream in state and input lanes (no divergent branch per stage)
@@ -483,8 +487,21 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NZ; ++i) g[i] = 0.0;
       const double ptl = L.hv[j];
       static_for<NX>([&](auto l) { fmac13_bc<decltype(l)::value>(y, hj, Pc, ptl, col[l]); });
+#if MPCB_P2_GVAR
+      // rows of G at the 10 variable directions by broadcasts; the 6 constant ones from Y alone:
+      // column e_p of [A|B] gives G[p][j] = Y[p][j], column e_v + hv e_p (hv = the tangent's
+      // h/6 * 6) gives G[v][j] = Y[v][j] + hv Y[p][j]
+#pragma unroll
+      for (int l = 0; l < NX; ++l) fmac10_var(g, col[l], y[l]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        g[p] = y[p];
+        g[6 + p] = fma(hv, y[p], y[6 + p]);
+      }
+#else
 #pragma unroll
       for (int l = 0; l < NX; ++l) fmac16_diag(g, col[l], y[l]);
+#endif
 #pragma unroll
       for (int i = 0; i < NZ; ++i) G[i] = g[i];
     } else {
