@@ -464,6 +464,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     constexpr int FD = BOX ? MPCB_AS_FDEPTH : MPCB_FWD_FDEPTH;
     constexpr int FL = KR2_W;
     T pv[FD][FL], pyb[FD], pgp[FD], pg[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) pg[i] = T(0);   // (a free component's row is never loaded)
     auto rload = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
       pyb[sl] = XU.at(k)[j * SS];
@@ -485,20 +487,30 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     if (fetch) gload(0);
     auto stage = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
-      const bool fixk = BOX && (((lowm | upm) >> k) & 1ull);   // input lanes: ju fixed at stage k
-      const uint64_t mfix = lane_mask(fixk);
+      // the lane's row of the dot below: a state lane's row of [A|B] (variable columns loaded,
+      // constant ones crow); an input lane's row of the stage Hessian with h_u (box), loaded where
+      // its component is fixed -- elsewhere the multiplier it yields is never read, so the row
+      // is whatever the slot held (no select on the fixed set), and without the box the input
+      // lanes' dot result is not used at all (no selects)
       T row[NZ];
+      if constexpr (BOX) {
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) row[i] = BOX ? csel(mfix, pg[i], T(0)) : T(0);
+        for (int t = 0; t < NVAR; ++t) row[var_col(t)] = csel(mst, pv[sl][t], pg[var_col(t)]);
 #pragma unroll
-      for (int t = 0; t < NVAR; ++t) row[var_col(t)] = csel(mst, pv[sl][t], row[var_col(t)]);
-      // constant columns of the state rows
+        for (int p = 0; p < 3; ++p) {
+          row[p] = csel(mst, crow[p], pg[p]);
+          row[6 + p] = csel(mst, crow[3 + p], pg[6 + p]);
+        }
+      } else {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        row[p] = csel(mst, crow[p], row[p]);
-        row[6 + p] = csel(mst, crow[3 + p], row[6 + p]);
+        for (int t = 0; t < NVAR; ++t) row[var_col(t)] = pv[sl][t];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          row[p] = crow[p];
+          row[6 + p] = crow[3 + p];
+        }
       }
-      const T r0 = csel(mst, iterate ? pgp[sl] : T(0), BOX ? csel(mfix, pg[NZ], T(0)) : T(0));
+      const T r0 = csel(mst, iterate ? pgp[sl] : T(0), BOX ? pg[NZ] : T(0));
       const T yb = pyb[sl];
       ASTAMP(4);
       // du = k + K dx (input lanes; dx_i broadcast from state lane i)
