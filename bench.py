@@ -382,6 +382,9 @@ def main():
     ap.add_argument('--backend', default='nccl', choices=('nccl', 'gloo'), help=argparse.SUPPRESS)
     ap.add_argument('--solver-stub', default=None, help=argparse.SUPPRESS)
     ap.add_argument('--dump-gather', default=None, help=argparse.SUPPRESS)
+    # rehearsal of the multi-rank path on a box with fewer GPUs than ranks: rank r binds
+    # cuda:(LOCAL_RANK % device_count) (the driver's scaling runs have one GPU per rank)
+    ap.add_argument('--share-gpus', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -401,16 +404,17 @@ def main():
     if 'WORLD_SIZE' in os.environ and args.gpus != world:
         raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
     cuda = args.solver_stub is None
-    if cuda and args.backend != 'nccl':
-        raise SystemExit('--backend gloo is for the CPU solver stub only')
+    if cuda and args.backend != 'nccl' and not args.share_gpus:
+        raise SystemExit('--backend gloo is for the CPU solver stub and the --share-gpus rehearsal only')
     if cuda:
-        torch.cuda.set_device(local)
+        gpu = local % torch.cuda.device_count() if args.share_gpus else local
+        torch.cuda.set_device(gpu)
         dev = torch.cuda.current_device()
     else:
         dev = 'cpu'
     if world > 1:
-        if cuda:
-            dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+        if cuda and args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device(f'cuda:{gpu}'))
         else:
             dist.init_process_group('gloo')
 
@@ -427,6 +431,7 @@ def main():
                'dtype': 'f32', 'path': r3['path'], 'roofline': roof3, 'bad_status': r3['bad']}
 
     if rank == 0:
+        coll = 'RCCL' if args.backend == 'nccl' else 'gloo'
         value, roof = summarize(w, r, world, args.steps)
         B, N = w['batch'], w['N']
         line = {
@@ -447,8 +452,9 @@ def main():
                                    + (', wind sweep, u0 histogram' if w['wind'] else ''),
                        'global_batch': B * world, 'horizon': N, 'path': r['path'],
                        'parallelism': f'instance-sharded x{world}'
-                                      + ((' + RCCL all_reduce(histogram)' if w['hist'] else ' + RCCL all_gather(u0)')
-                                         if world > 1 else '')},
+                                      + ((f' + {coll} all_reduce(histogram)' if w['hist'] else f' + {coll} all_gather(u0)')
+                                         if world > 1 else '')
+                                      + (' (ranks sharing GPUs: rehearsal)' if args.share_gpus else '')},
             'roofline': roof,
             'bad_status': r['bad'],
         }
