@@ -59,7 +59,8 @@ def compulsory_bytes(w) -> int:
 def cpu_baseline(w, budget_s=12.0):
     """The oracle timed on this host's cores on a bounded sample of the same workload: the plain-C
     restatement (oracle/c, OpenMP over instances, all cores this process may use) -- the
-    unconstrained path, the input box by the NumPy oracle's active set (c4), the wind force (c5)."""
+    unconstrained path, the input box by its primal-dual active set (c4), the wind force (c5) --
+    and, on a quarter of the budget, the same port on one thread (SURVEY §8 d: both figures)."""
     from oracle import c_oracle
     from oracle.inputs import make_inputs
     from oracle.ocp import OcpSpec
@@ -70,20 +71,24 @@ def cpu_baseline(w, budget_s=12.0):
     cores = int(os.environ.get('OMP_NUM_THREADS') or 0) or (
         len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count())
     c_oracle.load()
-    chunk = 4096 if not w['box'] else 2048
-    done, t_used, start = 0, 0.0, 0
-    while t_used < budget_s:
-        inp = make_inputs(w['name'], ids=np.arange(start, start + chunk, dtype=np.uint64), N=w['N'])
-        t0 = time.perf_counter()
-        c_oracle.solve(inp['x0'], inp['xref'], inp['uref'][:1], spec, nthreads=cores,
-                       want_traj=not w['hist'], wind=inp['wind'])
-        t_used += time.perf_counter() - t0
-        done += chunk
-        start += chunk
+    def timed(nthreads, chunk, budget):
+        done, t_used, start = 0, 0.0, 0
+        while t_used < budget:
+            inp = make_inputs(w['name'], ids=np.arange(start, start + chunk, dtype=np.uint64), N=w['N'])
+            t0 = time.perf_counter()
+            c_oracle.solve(inp['x0'], inp['xref'], inp['uref'][:1], spec, nthreads=nthreads,
+                           want_traj=not w['hist'], wind=inp['wind'])
+            t_used += time.perf_counter() - t0
+            done += chunk
+            start += chunk
+        return done, t_used
+    done, t_used = timed(cores, 4096 if not w['box'] else 2048, 0.75 * budget_s)
+    done1, t1 = timed(1, 256, 0.25 * budget_s)
     what = 'input-box active set' if w['box'] else ('wind' if w['wind'] else 'unconstrained')
     return dict(value=done / t_used, unit='solves/s', cores=cores, kind='port',
+                value_1thread=done1 / t1,
                 sample=f'{done} instances of {w["name"]} (N={w["N"]}, fp64, plain-C oracle oracle/c, '
-                       f'{what}, OpenMP) in {t_used:.1f} s')
+                       f'{what}, OpenMP) in {t_used:.1f} s; 1 thread: {done1} in {t1:.1f} s')
 
 
 class _DeviceClock:
