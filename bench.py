@@ -266,12 +266,13 @@ def dispatches_per_phase(B: int) -> int:
 def kernel_bytes(w, r, phase):
     """Algorithmic HBM bytes of the active-set kernel (c4, the only phase whose binding resource
     is memory): per forward stage the variable columns of [A|B] (12 x 10), K and k (4 x 13) and
-    (xbar, ubar) (16); per recomputed backward stage the [A|B] columns (120), the stage Hessian
-    rows it exports (4 x 17), K and k (52) and the value-function snapshot for restarts (12 x 13):
-    188 and 396 elements, counted from the kernel's own statistics (mpcb_qp_stats)."""
+    (xbar, ubar) (16); per recomputed backward stage the [A|B] columns (120), K and k (52) and the
+    value-function snapshot for restarts (P by symmetry and p: 78 + 12): 188 and 262 elements,
+    counted from the kernel's own statistics (mpcb_qp_stats).  (The Hessian rows of the fixed
+    components, written and read only where a component is fixed, are not counted.)"""
     esz = 8 if w['dtype'] == 'f64' else 4
     q = r['qp']
-    return esz * (188 * w['N'] * q['fwd_passes'] + 396 * q['bwd_stages'])
+    return esz * (188 * w['N'] * q['fwd_passes'] + 262 * q['bwd_stages'])
 
 
 def pmc_kernel(workload: str, kernel: str):
