@@ -71,23 +71,33 @@ __device__ unsigned long long g_astamps[12];
                        "v"(r[7]), "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11])
 #define ASQ_IN16(z, r) ASQ_IN12(z, r), "v"(r[12]), "v"(r[13]), "v"(r[14]), "v"(r[15])
 
-// acc[*] += sum_{l<12} bcast_l(z) * r[l]
+// fp32: acc[0] += sum_{l = 0 mod 4} ..., acc[1..3] = (their sums from zero): the first product of
+// accumulators 1..3 is a v_mul_f32_dpp instead of a v_fmac into a zeroed register (the zeroing
+// moves were ~5 % of a forward stage's instructions).  fp64 has no DPP form of v_mul_f64 (VOP3).
+#define ASQ_FIRST(M, mop) M(mop, 1, 4, 6, 1) M(mop, 2, 4, 7, 2) M(mop, 3, 4, 8, 3)
+#define ASQ_DOT12Z(M, op, mop)                                                                      \
+  M(op, 0, 4, 5, 0) ASQ_FIRST(M, mop) M(op, 0, 4, 9, 4) M(op, 1, 4, 10, 5) M(op, 2, 4, 11, 6)     \
+  M(op, 3, 4, 12, 7) M(op, 0, 4, 13, 8) M(op, 1, 4, 14, 9) M(op, 2, 4, 15, 10) M(op, 3, 4, 16, 11)
+#define ASQ_DOT16Z(M, op, mop) ASQ_DOT12Z(M, op, mop) M(op, 0, 4, 17, 12) M(op, 1, 4, 18, 13) M(op, 2, 4, 19, 14) M(op, 3, 4, 20, 15)
+#define ASQ_OUT4Z(acc) "+v"(acc[0]), "=&v"(acc[1]), "=&v"(acc[2]), "=&v"(acc[3])
+
+// acc[*] += sum_{l<12} bcast_l(z) * r[l]   (fp32: acc[1..3] need not be initialised)
 __device__ __forceinline__ void dot12(float (&acc)[4], float z, const float (&r)[12]) {
-  asm("s_nop 4\n\t" ASQ_DOT12(ASQ_I, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
+  asm("s_nop 4\n\t" ASQ_DOT12Z(ASQ_I, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN12(z, r));
 }
 __device__ __forceinline__ void dot12(double (&acc)[4], double z, const double (&r)[12]) {
   asm("s_nop 4\n\t" ASQ_DOT12(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
 }
-// acc[*] += sum_{l<16} bcast_l(z) * r[l]
+// acc[*] += sum_{l<16} bcast_l(z) * r[l]   (fp32: acc[1..3] need not be initialised)
 __device__ __forceinline__ void dot16(float (&acc)[4], float z, const float (&r)[16]) {
-  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_I, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+  asm("s_nop 4\n\t" ASQ_DOT16Z(ASQ_I, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN16(z, r));
 }
 __device__ __forceinline__ void dot16(double (&acc)[4], double z, const double (&r)[16]) {
   asm("s_nop 4\n\t" ASQ_DOT16(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
 }
-// acc[*] += sum_{l<16} |bcast_l(z) * r[l]|
+// acc[*] += sum_{l<16} |bcast_l(z) * r[l]|   (fp32: acc[1..3] need not be initialised)
 __device__ __forceinline__ void dot16abs(float (&acc)[4], float z, const float (&r)[16]) {
-  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f32_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+  asm("s_nop 4\n\t" ASQ_DOT16Z(ASQ_A, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN16(z, r));
 }
 __device__ __forceinline__ void dot16abs(double (&acc)[4], double z, const double (&r)[16]) {
   asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));

@@ -87,10 +87,21 @@ template <int n, class T> __device__ __forceinline__ T sel(const T* a, int j) {
   return sel_level<n, 0>(a, j);
 }
 
-// 1 / sqrt(x): fp32 sqrt + IEEE reciprocal; fp64 from the hardware estimate v_rsq_f64 refined
-// by two Newton steps (~1 ulp, a fraction of the instructions of sqrt + an IEEE division).
-// A non-positive pivot still yields NaN/inf, which the callers' status checks catch.
-__device__ __forceinline__ float inv_sqrt(float x) { return 1.0f / sqrtf(x); }
+// 1 / sqrt(x) from the hardware estimate v_rsq refined by Newton steps: fp32 one (~1 ulp; sqrtf and
+// an IEEE division were ~13 instructions per pivot), fp64 two (~1 ulp, a fraction of the
+// instructions of sqrt + an IEEE division).  A non-positive pivot still yields NaN/inf, which the
+// callers' status checks catch.  MPCB_IEEE_DIV=1 restores sqrt + division in fp32.
+#ifndef MPCB_IEEE_DIV
+#define MPCB_IEEE_DIV 0
+#endif
+__device__ __forceinline__ float inv_sqrt(float x) {
+#if MPCB_IEEE_DIV
+  return 1.0f / sqrtf(x);
+#else
+  const float r = __builtin_amdgcn_rsqf(x);
+  return r * fmaf(-0.5f * x * r, r, 1.5f);
+#endif
+}
 __device__ __forceinline__ double inv_sqrt(double x) {
   double r = __builtin_amdgcn_rsq(x);
 #pragma unroll
