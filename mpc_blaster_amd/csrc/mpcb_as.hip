@@ -597,7 +597,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       if (!stl) a.u0[b * NU + ju] = us[ju];
       u0fin = true;
 #pragma unroll
-      for (int m = 0; m < NU; ++m) u0fin = u0fin && (us[m] - us[m] == T(0));
+      for (int m = 0; m < NU; ++m) u0fin = u0fin && isfin(us[m]);
     };
     if (!stage_out && write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
     if (!BOX && stage_out && write) flush_out();
@@ -653,7 +653,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       T u0c[NU];
       load_vec<NU>(a.u0 + b * NU, u0c);
 #pragma unroll
-      for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+      for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
     }
     // the QP status of the unconstrained pass (P2 wrote it) carries over
     const int32_t st0 = a.status[b];

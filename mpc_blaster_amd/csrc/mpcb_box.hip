@@ -485,7 +485,7 @@ __device__ __forceinline__ void box_body(const SplitArgs<T>& a) {
     load_vec<NU>(a.u0 + b * NU, u0c);
     bool fin = true;
 #pragma unroll
-    for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+    for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
     // the QP status of the unconstrained pass (P2 wrote it) carries over
     const int32_t st0 = MODE != PASS_SMALL ? a.status[b] : MPCB_STATUS_OK;
     a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);

@@ -69,6 +69,11 @@ template <class T> __device__ __forceinline__ T csel(uint64_t m, T a, T b) {
 }
 __device__ __forceinline__ uint64_t lane_mask(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 
+// x is finite (one v_cmp_class).  Not (x - x) == 0: when x is a product formed in the same
+// expression, FMA contraction turns x - x into fma(a, b, -x) = the product's rounding error, and
+// a finite x then reads as non-finite (it did, in the 17/6 interior point's step test).
+template <class T> __device__ __forceinline__ bool isfin(T x) { return __builtin_isfinite(x); }
+
 // a[j] (0 <= j < n <= 16) for a register array: a bit-tree of csel on the bits of j.
 template <int n, int bit, class T> __device__ __forceinline__ T sel_level(const T* a, int j) {
   if constexpr (n == 1) {

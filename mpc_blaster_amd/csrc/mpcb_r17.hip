@@ -224,8 +224,9 @@ struct SRow {
              r.w.IX[(int64_t)k * 4 * NX17 + i], r.w.IX[(int64_t)k * 4 * NX17 + NX17 + i],
              r.w.IX[(int64_t)k * 4 * NX17 + 2 * NX17 + i], r.w.IX[(int64_t)k * 4 * NX17 + 3 * NX17 + i]) {}
   __device__ __forceinline__ void barrier(T smu, T& D, T& d) const {
-    D = ll / sl + lu / su;
-    d = -smu * (T(1) / sl - T(1) / su) + (ll / sl) * rl - (lu / su) * ru;
+    const T isl = recip(sl), isu = recip(su);
+    D = ll * isl + lu * isu;
+    d = -smu * (isl - isu) + (ll * isl) * rl - (lu * isu) * ru;
   }
 };
 
@@ -423,7 +424,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       }
       if (ipm) {
         const T sl = ic.du - (lbm - cu.ub), su = (ubm - cu.ub) - ic.du;
-        T D = ic.ll / sl + ic.lu / su, d = -smu * (T(1) / sl - T(1) / su);
+        const T isl = recip(sl), isu = recip(su);
+        T D = ic.ll * isl + ic.lu * isu, d = -smu * (isl - isu);
         if constexpr (POLC) {
           const bool act = ic.lu != T(0);
           const T bnd = ic.lu < T(0) ? lbm - cu.ub : ubm - cu.ub;
@@ -707,8 +709,9 @@ __device__ __forceinline__ void backward_corr(const Ctx<T>& r, T smu) {
 
 // complementarity targets of a row for Mehrotra's corrector: t = sigma mu - Delta s_a Delta lambda_a
 template <class T>
-__device__ __forceinline__ void targets(T smu, T sl, T su, T ll, T lu, T dsl_a, T dsu_a, T& tl, T& tu) {
-  const T dll_a = (-ll * sl - ll * dsl_a) / sl, dlu_a = (-lu * su - lu * dsu_a) / su;
+__device__ __forceinline__ void targets(T smu, T sl, T su, T ll, T lu, T dsl_a, T dsu_a, T& tl, T& tu,
+                                        T isl, T isu) {
+  const T dll_a = (-ll * sl - ll * dsl_a) * isl, dlu_a = (-lu * su - lu * dsu_a) * isu;
   tl = smu - dsl_a * dll_a;
   tu = smu - dsu_a * dlu_a;
 }
@@ -796,7 +799,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     }
     if (in) {
       const T uo = cr.ubm + du;
-      fin = fin && ((uo - uo) == T(0));
+      fin = fin && isfin(uo);
     }
     // dx' = [A|B] (dx, du) + gap: lanes broadcast their z value (du on input lanes); row 8 as a
     // row sum of the lanes' own terms
@@ -806,7 +809,7 @@ __device__ __forceinline__ bool forward(const Ctx<T>& r, T dxs, T dx8, bool writ
     const T acc8 = sum16(cr.ab8o * zb, (gaps ? cr.g8 : T(0)) + cr.c88 * dx8);
     dxs = acc;
     dx8 = acc8;
-    fin = fin && ((dxs - dxs) == T(0)) && ((dx8 - dx8) == T(0));
+    fin = fin && isfin(dxs) && isfin(dx8);
     // refill this slot FD stages ahead, unconditionally (a clamped stage index past the end): a
     // refill under a branch makes the count of loads in flight path-dependent, and the
     // compiler then waits for every load (vmcnt(1)) at the top of each stage
@@ -975,12 +978,12 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           xo[s] = r.w.XB[(int64_t)k * NX17 + s] + xs;
           if (t == 0) xo[OM] = r.w.XB[(int64_t)k * NX17 + OM] + x8;
         }
-        fin = fin && ((xs - xs) == T(0)) && ((x8 - x8) == T(0));
+        fin = fin && isfin(xs) && isfin(x8);
         if (in && k < N) {
           T duk = r.w.IP[(int64_t)k * 18 + m];
           if (POLC && pst == 2) duk = duk + r.w.DDU[(int64_t)k * NU17 + m];
           const T uo = r.w.UB[(int64_t)k * NU17 + m] + duk;
-          fin = fin && ((uo - uo) == T(0));
+          fin = fin && isfin(uo);
           if (valid && a.U) a.U[(b * (int64_t)N + k) * NU17 + m] = uo;
           if (valid && k == 0) a.u0[b * NU17 + m] = uo;
         }
@@ -1159,7 +1162,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       // the affine step to the boundary alpha_a, mu_a = (S0 + alpha_a S1 + alpha_a^2 S2) / (2 rows),
       // and per input row w = 1/s_l - 1/s_u, c = Delta s_a Delta lambda_a / s_l - (upper) into DC
       // (the state entries zero: no state rows here)
-      T aa = T(1), S0 = T(0), S1 = T(0), S2 = T(0);
+      // (ratio tests as the largest -dv / v over the rows, by the rows' reciprocals: aa = 1 /
+      // max(1, that), no division per row)
+      T raa = T(1), S0 = T(0), S1 = T(0), S2 = T(0);
       if (in && !parked) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
@@ -1167,18 +1172,16 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T* ip = r.w.IP + (int64_t)k * 18;
           const T d = r.wm.DAU[(int64_t)k * NU17 + m];
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m], ll = ip[6 + m], lu = ip[12 + m];
+          const T isl = recip(sl), isu = recip(su);
           const T dsl = d, dsu = -d;
-          const T dll = (-ll * sl - ll * dsl) / sl, dlu = (-lu * su - lu * dsu) / su;
-          if (dsl < T(0)) aa = fmin(aa, -sl / dsl);
-          if (dsu < T(0)) aa = fmin(aa, -su / dsu);
-          if (dll < T(0)) aa = fmin(aa, -ll / dll);
-          if (dlu < T(0)) aa = fmin(aa, -lu / dlu);
+          const T dll = (-ll * sl - ll * dsl) * isl, dlu = (-lu * su - lu * dsu) * isu;
+          raa = fmax(raa, fmax(fmax(-dsl * isl, -dsu * isu), fmax(-dll * recip(ll), -dlu * recip(lu))));
           S0 += sl * ll + su * lu;
           S1 += sl * dll + ll * dsl + su * dlu + lu * dsu;
           S2 += dsl * dll + dsu * dlu;
           T* dc = r.wm.DC + (int64_t)k * WsM17<T>::DC_N + NX17 + m;
-          dc[0] = T(1) / sl - T(1) / su;
-          dc[24] = dsl * dll / sl - dsu * dlu / su;
+          dc[0] = isl - isu;
+          dc[24] = dsl * dll * isl - dsu * dlu * isu;
         }
       }
       if (!parked) {
@@ -1193,7 +1196,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           dc[24 + OM] = T(0);
         }
       }
-      aa = row_min(aa);
+      const T aa = T(1) / row_max(raa);
       const T mu_a = (row_sum(S0) + aa * row_sum(S1) + aa * aa * row_sum(S2)) / (T(2) * rows);
       const T ratio = mu_a / mu;
       const T sig3 = ratio * ratio * ratio;
@@ -1210,7 +1213,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       QSTAMP(9);
       }
       // step length: fraction tau to the boundary, primal and dual, common to the instance
-      T amax = T(1) / T(IPM17_TAU);
+      // (the ratio tests as in the predictor: the largest -dv / v, from tau; amax = 1 / that)
+      T ram = T(IPM17_TAU);
       bool dfin = true;   // a finite direction from strictly positive slacks
       if (in && !parked) {
 #pragma unroll 4
@@ -1220,17 +1224,15 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T d = r.w.DDU[(int64_t)k * NU17 + m];
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
           const T ll = ip[6 + m], lu = ip[12 + m];
+          const T isl = recip(sl), isu = recip(su);
           T tl = smu, tu = smu;
           if constexpr (MEH) {
             const T da = r.wm.DAU[(int64_t)k * NU17 + m];
-            targets(smu, sl, su, ll, lu, da, -da, tl, tu);
+            targets(smu, sl, su, ll, lu, da, -da, tl, tu, isl, isu);
           }
-          const T dll = (tl - ll * sl - ll * d) / sl, dlu = (tu - lu * su + lu * d) / su;
-          dfin = dfin && sl > T(0) && su > T(0) && (d - d) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
-          if (d < T(0)) amax = fmin(amax, -sl / d);
-          if (d > T(0)) amax = fmin(amax, su / d);
-          if (dll < T(0)) amax = fmin(amax, -ll / dll);
-          if (dlu < T(0)) amax = fmin(amax, -lu / dlu);
+          const T dll = (tl - ll * sl - ll * d) * isl, dlu = (tu - lu * su + lu * d) * isu;
+          dfin = dfin && sl > T(0) && su > T(0) && isfin(d) && isfin(dll) && isfin(dlu);
+          ram = fmax(ram, fmax(fmax(-d * isl, d * isu), fmax(-dll * recip(ll), -dlu * recip(lu))));
         }
       }
       if (sbox && !parked) {
@@ -1238,19 +1240,17 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const SRow<T> sr(r, k, i);
           const T dy = r.w.DDX[(int64_t)k * NX17 + i];
           const T dsl = dy + sr.rl, dsu = sr.ru - dy;
-          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
-          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
-          dfin = dfin && (dsl - dsl) == T(0) && (dsu - dsu) == T(0) && (dll - dll) == T(0) && (dlu - dlu) == T(0);
-          if (dsl < T(0)) amax = fmin(amax, -sr.sl / dsl);
-          if (dsu < T(0)) amax = fmin(amax, -sr.su / dsu);
-          if (dll < T(0)) amax = fmin(amax, -sr.ll / dll);
-          if (dlu < T(0)) amax = fmin(amax, -sr.lu / dlu);
+          const T isl = recip(sr.sl), isu = recip(sr.su);
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) * isl;
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) * isu;
+          dfin = dfin && isfin(dsl) && isfin(dsu) && isfin(dll) && isfin(dlu);
+          ram = fmax(ram, fmax(fmax(-dsl * isl, -dsu * isu), fmax(-dll * recip(sr.ll), -dlu * recip(sr.lu))));
         };
 #pragma unroll 4
         for (int k = 1; k < N; ++k) step_row(k, s);
         for (int k = 1 + t; k < N; k += LN) step_row(k, OM);
       }
-      amax = row_min(amax);
+      const T amax = T(1) / row_max(ram);
       QSTAMP(3);
       const int dbad = row_or(dfin ? 0 : 1);
       // (a finished instance skips the updates: its Newton step may be non-finite)
@@ -1279,12 +1279,13 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T d = r.w.DDU[(int64_t)k * NU17 + m];
           const T sl = ip[m] - (lbm - ubk), su = (ubm - ubk) - ip[m];
           const T ll = ip[6 + m], lu = ip[12 + m];
+          const T isl = recip(sl), isu = recip(su);
           T tl = smu, tu = smu;
           if constexpr (MEH) {
             const T da = r.wm.DAU[(int64_t)k * NU17 + m];
-            targets(smu, sl, su, ll, lu, da, -da, tl, tu);
+            targets(smu, sl, su, ll, lu, da, -da, tl, tu, isl, isu);
           }
-          const T dll = (tl - ll * sl - ll * d) / sl, dlu = (tu - lu * su + lu * d) / su;
+          const T dll = (tl - ll * sl - ll * d) * isl, dlu = (tu - lu * su + lu * d) * isu;
           const T dun = ip[m] + alpha * d, lln = ll + alpha * dll, lun = lu + alpha * dlu;
           ip[m] = dun;
           ip[6 + m] = lln;
@@ -1297,8 +1298,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const SRow<T> sr(r, k, i);
           const T dy = r.w.DDX[(int64_t)k * NX17 + i];
           const T dsl = dy + sr.rl, dsu = sr.ru - dy;
-          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) / sr.sl;
-          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) / sr.su;
+          const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) * recip(sr.sl);
+          const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) * recip(sr.su);
           T* ix = r.w.IX + (int64_t)k * 4 * NX17 + i;
           SRow<T> nr = sr;   // the row after the step (dx moves by alpha ddx in the next backward)
           nr.y = sr.y + alpha * dy;

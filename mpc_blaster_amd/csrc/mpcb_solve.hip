@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(64) MPCB_WAVES solve_kernel(SolveArgs<T> a) {
       load_vec<NU>(a.u0 + b * NU, u0c);
       bool fin = true;
 #pragma unroll
-      for (int m = 0; m < NU; ++m) fin = fin && (u0c[m] - u0c[m] == T(0));
+      for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
       a.status[b] = fin ? st : MPCB_STATUS_NAN;
     }
     __syncthreads();

@@ -652,7 +652,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     // rollout mode without trajectories: dx_0 = 0 so u0 = ubar_0 + kff_0
     const T u = cyb + kff0;   // cyb = own component of (xbar_0 | ubar_0)
     a.u0[b * NU + ju] = u;
-    const bool fin = (u - u) == T(0);
+    const bool fin = isfin(u);
     if (!fin) a.status[b] = MPCB_STATUS_NAN;
   }
 }
@@ -786,7 +786,7 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
       for (int m = 0; m < NU; ++m) {
         uo[m] = ub[m] + du[m];
         row[NX + m] = uo[m];
-        fin = fin && (uo[m] - uo[m] == T(0));
+        fin = fin && isfin(uo[m]);
       }
       if (k == 0 && valid) store_vec<NU>(a.u0 + b * NU, uo);
     }
@@ -827,7 +827,7 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
     }
   }
 #pragma unroll
-  for (int i = 0; i < NX; ++i) fin = fin && (dx[i] - dx[i] == T(0));
+  for (int i = 0; i < NX; ++i) fin = fin && isfin(dx[i]);
   if (valid && !fin) a.status[b] = MPCB_STATUS_NAN;
 }
 
