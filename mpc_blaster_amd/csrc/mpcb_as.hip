@@ -632,8 +632,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     } else {
       changed = 0;
     }
-    // (the first masked pass is complete: P2 stored no snapshots)
-    kc = changed ? (it == 0 ? N - 1 : 63 - __clzll(changed)) : -1;
+    // restart at kc + 1 from the snapshot there: the last pass that recomputed that stage, or
+    // (never recomputed: its active set is still empty) P2's unconstrained pass
+    kc = changed ? 63 - __clzll(changed) : -1;
     if (BOX && stage_out && write && (gconv || it + 1 >= a.max_as_iter)) flush_out();
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     if (!done && gconv) done = true;

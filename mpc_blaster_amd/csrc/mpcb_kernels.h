@@ -83,7 +83,8 @@ constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 //   GH2  [4][20]   row m of the stage Hessian's input rows (16 entries), slot 16 = h_u[m]; written
 //                  by the active-set kernel's masked backward, only where component m is fixed
 //   PS2  [12][8]   P_k packed by symmetry: lane j keeps P[j][(j + d) % 12], d = 0..6, and p_k[j]
-//                  in slot 7 (84 slots for its 78 distinct entries)
+//                  in slot 7 (84 slots for its 78 distinct entries); written by P2's unconstrained
+//                  pass and by every stage the active-set kernel recomputes (its restart points)
 constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
 constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, GH2_REC = 4 * 20,
               PS2_REC = 12 * PS2_W;

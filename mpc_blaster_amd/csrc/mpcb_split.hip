@@ -621,6 +621,20 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     pj = pn;
     if (k > 0) commit(buf ^ 1);
     wave_lds_sync();
+    if (EXPORT && a.PS && valid && j < NX && k > 0) {
+      // box path: the value function P_k, p_k packed by symmetry (mpcb_kernels.h PS2), so the
+      // active-set kernel's first masked pass restarts above the highest violated stage instead
+      // of recomputing the whole horizon; slot d of lane j is P[j][(j + d) % 12], published by
+      // lane max(j, o) above
+      T ps[PS2_W];
+#pragma unroll
+      for (int d = 0; d < 7; ++d) {
+        const int o = j + d < NX ? j + d : j + d - NX;
+        ps[d] = L.X[(o > j ? o : j) * XS + (o > j ? j : o)];
+      }
+      ps[7] = pn;
+      stv<T, PS2_W>(rec2(a.PS, k, PS2_REC, nb, c, N, a.imajor) + j * PS2_W, ps);
+    }
     STAMP(8);
 #if MPCB_P2_PCSEL
     {   // unconditional LDS reads + lane-mask selects (no exec-masked branch per entry)
