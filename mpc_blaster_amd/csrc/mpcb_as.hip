@@ -123,6 +123,7 @@ template <int L> __device__ __forceinline__ unsigned bcu(unsigned v) {
 }
 template <int L> __device__ __forceinline__ int bc(int v) { return (int)bcu<L>((unsigned)v); }
 template <int L> __device__ __forceinline__ float bc(float v) { return __uint_as_float(bcu<L>(__float_as_uint(v))); }
+template <int L> __device__ __forceinline__ unsigned bc(unsigned v) { return bcu<L>(v); }
 template <int L> __device__ __forceinline__ uint64_t bc(uint64_t v) {
   return ((uint64_t)bcu<L>((unsigned)(v >> 32)) << 32) | bcu<L>((unsigned)v);
 }
@@ -157,8 +158,21 @@ template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int6
 constexpr int OUT_NMAX = 64;   // longer horizons store directly
 template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
 
-template <class T, bool BOX>
+// Stage masks (active sets, violations: bit k = stage k) of a horizon N <= 32 in 32-bit registers
+// (W32: half the VALU of every mask shift / or in the stage loops), else 64-bit.
+template <bool W32> struct Masks {
+  using M = std::conditional_t<W32, uint32_t, uint64_t>;
+  static constexpr int WB = W32 ? 32 : 64;
+  __device__ static __forceinline__ int popc(M v) { if constexpr (W32) return __builtin_popcount(v); else return __popcll(v); }
+  __device__ static __forceinline__ int ffs(M v) { if constexpr (W32) return __builtin_ffs((int)v); else return __ffsll((long long)v); }
+  __device__ static __forceinline__ int clz(M v) { if constexpr (W32) return __builtin_clz(v); else return __clzll(v); }
+};
+
+template <class T, bool BOX, bool W32 = false>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
+  using Mk = Masks<W32>;
+  using M = typename Mk::M;
+  constexpr int WB = Mk::WB;
   __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
   extern __shared__ __attribute__((aligned(16))) unsigned char as_dyn[];
   const int lane = threadIdx.x;
@@ -210,7 +224,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   }
   const T* xrN = xr + (int64_t)N * NX;
 
-  uint64_t lowm = 0, upm = 0;   // input lanes: active sets of component ju, bit k = stage k
+  M lowm = 0, upm = 0;          // input lanes: active sets of component ju, bit k = stage k
   bool done = false;
   int32_t st = MPCB_STATUS_OK;
   int best = 0x7fffffff, pcount = 3;
@@ -340,7 +354,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         // unmasked input row of a component fixed at this stage: the forward's multiplier.  (Where
         // the component is free the forward never reads the row, and a stage whose fixed set
         // changes is recomputed -- and its row written -- before the next forward pass.)
-        if (act && valid && !stl && (((lowm | upm) >> k) & 1ull)) {
+        if (act && valid && !stl && (((lowm | upm) >> k) & 1u)) {
           T gr[20];
 #pragma unroll
           for (int i = 0; i < NZ; ++i) gr[i] = G[i];
@@ -360,7 +374,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           Hux_t[m] = G[NX + m];
         });
         {
-          const bool lo = (lowm >> k) & 1ull, hi = (upm >> k) & 1ull;
+          const bool lo = (lowm >> k) & 1u, hi = (upm >> k) & 1u;
           const int fx_own = (!stl && (lo || hi)) ? 1 : 0;
           const T dl_own = lo ? (lbm - yb) : (hi ? (ubm - yb) : T(0));   // input lanes: yb = ubar
           int fixed[NU];
@@ -455,7 +469,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     }
 
     // ------------------------------------------------ forward pass, multipliers, violations
-    uint64_t vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
+    M vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
     const bool write = valid && !done;
     // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
     const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
@@ -486,7 +500,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       if (iterate) pgp[sl] = GP.at(k)[jx * SS];   // state lanes: gap_jx (input lanes: unused)
     };
     auto gload = [&](int k) {
-      if (BOX && (((lowm | upm) >> k) & 1ull)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
+      if (BOX && (((lowm | upm) >> k) & 1u)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
     };
     // a converged group rides along with its wave's other groups: its loads are skipped and its
     // results (garbage) neither written nor used
@@ -549,7 +563,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       T acc[4] = {r0, T(0), T(0), T(0)};
       dot16(acc, zj, row);
       const T v = sum4(acc);
-      const bool lo = !stl && ((lowm >> k) & 1ull), hi = !stl && ((upm >> k) & 1ull);
+      const bool lo = !stl && ((lowm >> k) & 1u), hi = !stl && ((upm >> k) & 1u);
       T tol_mu = T(0);
       if (BOX && __builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
         T aa[4] = {T(fabs(r0)), T(0), T(0), T(0)};
@@ -560,10 +574,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         const bool fr = !(lo || hi);
         const T mu = v;
         // violations beyond the rounding noise of u and mu (see mpcb_box.hip)
-        vlo |= (uint64_t)(fr && yo < lbm - tol_u) << k;
-        vhi |= (uint64_t)(fr && yo > ubm + tol_u) << k;
-        vfl |= (uint64_t)(lo && mu < -tol_mu) << k;
-        vfu |= (uint64_t)(hi && mu > tol_mu) << k;
+        vlo |= (M)(fr && yo < lbm - tol_u) << k;
+        vhi |= (M)(fr && yo > ubm + tol_u) << k;
+        vfl |= (M)(lo && mu < -tol_mu) << k;
+        vfu |= (M)(hi && mu > tol_mu) << k;
       } else {
         zj = v;
       }
@@ -604,9 +618,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     if constexpr (!BOX) break;
 
     // ------------------------------------------------ active-set update (Kim-Park)
-    const uint64_t V = vlo | vhi | vfl | vfu;
-    const int cnt = stl ? 0 : __popcll(V);
-    const int firstk = (!stl && V) ? __ffsll((long long)V) - 1 : 64;
+    const M V = vlo | vhi | vfl | vfu;
+    const int cnt = stl ? 0 : Mk::popc(V);
+    const int firstk = (!stl && V) ? Mk::ffs(V) - 1 : WB;
     int nV, first;
     {
       const int c0 = bc<NX + 0>(cnt), c1 = bc<NX + 1>(cnt), c2 = bc<NX + 2>(cnt), c3 = bc<NX + 3>(cnt);
@@ -620,12 +634,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     const bool full = (nV < best) || (pcount > 0);
     pcount = (nV < best) ? 3 : (full ? pcount - 1 : pcount);
     best = nV < best ? nV : best;
-    const uint64_t selm =
-        full ? V : ((first < 64 * NU && (first % NU) == ju && !stl) ? (1ull << (first / NU)) : 0ull);
-    const uint64_t nlow = (lowm | (selm & vlo)) & ~(selm & vfl);
-    const uint64_t nup = (upm | (selm & vhi)) & ~(selm & vfu);
-    const uint64_t diff = stl ? 0ull : ((nlow ^ lowm) | (nup ^ upm));
-    uint64_t changed = (bc<NX + 0>(diff) | bc<NX + 1>(diff)) | (bc<NX + 2>(diff) | bc<NX + 3>(diff));
+    const M selm = full ? V : ((first < WB * NU && (first % NU) == ju && !stl) ? (M(1) << (first / NU)) : M(0));
+    const M nlow = (lowm | (selm & vlo)) & ~(selm & vfl);
+    const M nup = (upm | (selm & vhi)) & ~(selm & vfu);
+    const M diff = stl ? M(0) : ((nlow ^ lowm) | (nup ^ upm));
+    M changed = (bc<NX + 0>(diff) | bc<NX + 1>(diff)) | (bc<NX + 2>(diff) | bc<NX + 3>(diff));
     if (!done && !gconv) {
       lowm = nlow;
       upm = nup;
@@ -634,7 +647,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     }
     // restart at kc + 1 from the snapshot there: the last pass that recomputed that stage, or
     // (never recomputed: its active set is still empty) P2's unconstrained pass
-    kc = changed ? 63 - __clzll(changed) : -1;
+    kc = changed ? WB - 1 - Mk::clz(changed) : -1;
     if (BOX && stage_out && write && (gconv || it + 1 >= a.max_as_iter)) flush_out();
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     if (!done && gconv) done = true;
@@ -668,19 +681,25 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 
 }  // namespace asq
 
+template <bool W32>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS_WAVES, 8)))
-as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true>(a); }
-__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true>(a); }
+as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true, W32>(a); }
+template <bool W32>
+__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true, W32>(a); }
 template <class T>
 __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false>(a); }
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(as_kernel_f32, dim3(g), dim3(64), lds, st, a);
-  else
-    hipLaunchKernelGGL(as_kernel_f64, dim3(g), dim3(64), lds, st, a);
+  const bool w32 = a.N <= 32;   // (the stage masks fit 32 bits)
+  if constexpr (sizeof(T) == 4) {
+    if (w32) hipLaunchKernelGGL(as_kernel_f32<true>, dim3(g), dim3(64), lds, st, a);
+    else hipLaunchKernelGGL(as_kernel_f32<false>, dim3(g), dim3(64), lds, st, a);
+  } else {
+    if (w32) hipLaunchKernelGGL(as_kernel_f64<true>, dim3(g), dim3(64), lds, st, a);
+    else hipLaunchKernelGGL(as_kernel_f64<false>, dim3(g), dim3(64), lds, st, a);
+  }
   return hipGetLastError();
 }
 // forward pass of the unconstrained small-chunk path from P2's row-major exports (ABT2, KR2)
