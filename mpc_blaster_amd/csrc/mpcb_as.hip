@@ -183,25 +183,39 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   const bool stl = j < NX;                          // state lane (else input lane ju)
   const uint64_t mst = lane_mask(stl);
   T* const PX = lds_px[q];
-  const int64_t c_raw = (int64_t)blockIdx.x * GROUPS + q;
-  const bool valid = c_raw < a.nb;
-  const int64_t c = valid ? c_raw : a.nb - 1;       // inactive groups shadow the last instance
   const int64_t nb = a.nb;
-  const int64_t b = a.b0 + c;
   const int N = a.N;
   const T h = a.h;
   const Weights<T>& W = *a.W;
   const bool iterate = a.mode == MPCB_MODE_ITERATE;
-  const T* xr = a.xref + b * a.xref_sb;
-  const T* ur = a.uref + b * a.uref_sb;
   const T lbm = W.lbu[ju], ubm = W.ubu[ju];
   constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
   const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
   const int64_t nq = (nb + SS - 1) / SS;
-  const Arr<T> XU = arr(a.XU, XU_REC, nq, c), GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
-  const Arr<T> AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c, N, a.imajor), ABT = arr2(a.ABT, ABT2_REC, nq, c, N, a.imajor);
-  const Arr<T> GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c, N, a.imajor), KR = arr2(a.KR, KR2_REC, nq, c, N, a.imajor);
-  const Arr<T> PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c, N, a.imajor);
+  // The group's instance and its workspace records.  Box kernel with a work counter (a.as_queue):
+  // the grid holds the waves the machine keeps resident, and a group whose instance finished
+  // takes the next one from the counter, so a wave does not carry three idle groups while its
+  // slowest instance finishes (3.8 active-set passes per instance, 5.2 per wave with fixed quads).
+  bool valid;
+  int64_t c, b;
+  const T *xr, *ur, *xrN;
+  Arr<T> XU, GP, AB, ABT, GH, KR, PS;
+  auto bind = [&](int64_t c_raw) {
+    valid = c_raw < nb;
+    c = valid ? c_raw : nb - 1;       // an empty group shadows the last instance
+    b = a.b0 + c;
+    xr = a.xref + b * a.xref_sb;
+    ur = a.uref + b * a.uref_sb;
+    xrN = xr + (int64_t)N * NX;
+    XU = arr(a.XU, XU_REC, nq, c);
+    GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
+    AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c, N, a.imajor);
+    ABT = arr2(a.ABT, ABT2_REC, nq, c, N, a.imajor);
+    GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c, N, a.imajor);
+    KR = arr2(a.KR, KR2_REC, nq, c, N, a.imajor);
+    PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c, N, a.imajor);
+  };
+  bind((int64_t)blockIdx.x * GROUPS + q);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
   // the stage cost of direction j, when a backward stage needs it
@@ -222,19 +236,38 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     crow[p] = (jx == p) ? T(1) : T(0);
     crow[3 + p] = ((jx == 6 + p) ? T(1) : T(0)) + ((jx == p) ? h : T(0));
   }
-  const T* xrN = xr + (int64_t)N * NX;
 
   M lowm = 0, upm = 0;          // input lanes: active sets of component ju, bit k = stage k
-  bool done = false;
+  bool done = !valid;           // (box: the group has no instance left)
   int32_t st = MPCB_STATUS_OK;
   int best = 0x7fffffff, pcount = 3;
   int n_fwd = 0, n_bst = 0;
-  int kc = N - 1;               // highest stage whose active set changed (group-uniform)
+  int kc = -1;                  // highest stage whose active set changed (group-uniform)
+  int git = 0;                  // passes of the group's current instance
   bool u0fin = true;            // u0 of the flushed (final) pass is finite (staged outputs)
+  const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
+  // an instance's outcome: the QP status of the unconstrained pass (P2 wrote it) carries over
+  auto finish = [&]() {
+    if (valid && j == NX) {
+      bool fin = u0fin;
+      if (!stage_out) {   // direct stores
+        T u0c[NU];
+        load_vec<NU>(a.u0 + b * NU, u0c);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
+      }
+      const int32_t st0 = a.status[b];
+      a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
+      if (BOX && a.qp_stats) {
+        a.qp_stats[2 * b] = n_fwd;
+        a.qp_stats[2 * b + 1] = n_bst;
+      }
+    }
+  };
 #ifdef MPCB_STAMPS
   unsigned long long ast_prev = __builtin_amdgcn_s_memtime(), ast_acc[12] = {};
 #endif
-  for (int it = 0;; ++it) {
+  for (;;) {
 #ifdef MPCB_STAMPS
     ast_acc[8] += 1;
 #endif
@@ -244,11 +277,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       const int o = __builtin_amdgcn_readlane(kc, g * 16);
       kmax = o > kmax ? o : kmax;
     }
-    if (it > 0 && !done && kc >= 0) n_bst += kc + 1;
+    if (git > 0 && !done && kc >= 0) n_bst += kc + 1;
     if (!done) ++n_fwd;
     // ------------------------------------------------ masked Riccati over the cached [A|B]
     ASTAMP(7);
-    if (BOX && it > 0 && kmax >= 0) {
+    if (BOX && kmax >= 0) {   // (a group in its first pass has kc = -1)
 #ifdef MPCB_STAMPS
       ast_acc[9] += kmax + 1;
 #endif
@@ -472,7 +505,6 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     M vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
     const bool write = valid && !done;
     // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
-    const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
     T* const xs = reinterpret_cast<T*>(as_dyn) + q * out_elems<T>(N);   // X rows, then U rows
     T* const us = xs + (N + 1) * NX;
     T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
@@ -648,35 +680,40 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     // restart at kc + 1 from the snapshot there: the last pass that recomputed that stage, or
     // (never recomputed: its active set is still empty) P2's unconstrained pass
     kc = changed ? WB - 1 - Mk::clz(changed) : -1;
-    if (BOX && stage_out && write && (gconv || it + 1 >= a.max_as_iter)) flush_out();
+    // the instance is finished: converged, or the pass cap
+    const bool fin_now = write && (gconv || git + 1 >= a.max_as_iter);
+    if (stage_out && fin_now) flush_out();
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
-    if (!done && gconv) done = true;
-    if (__all(done || !valid)) break;
-    if (it + 1 >= a.max_as_iter) {
-      if (!done) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
-      break;
+    ++git;
+    if (fin_now) {
+      if (!gconv) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+      finish();
+      // the next instance of the chunk (lane 0 of the group draws it), else the group stays empty
+      int nxt = (int)nb;
+      if (a.as_queue) {
+        if (j == 0) nxt = (int)gridDim.x * GROUPS + atomicAdd(a.as_queue, 1);
+        nxt = bc<0>(nxt);
+      }
+      bind(nxt);
+      lowm = upm = 0;
+      st = MPCB_STATUS_OK;
+      best = 0x7fffffff;
+      pcount = 3;
+      n_fwd = n_bst = 0;
+      kc = -1;
+      git = 0;
+      u0fin = true;
+      done = !valid;
+    } else if (!valid) {
+      done = true;
     }
+    if (__all(done)) break;
   }
 #ifdef MPCB_STAMPS
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
 #endif
-  if (valid && j == NX) {
-    bool fin = u0fin;
-    if (!(N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0)) {   // direct stores
-      T u0c[NU];
-      load_vec<NU>(a.u0 + b * NU, u0c);
-#pragma unroll
-      for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
-    }
-    // the QP status of the unconstrained pass (P2 wrote it) carries over
-    const int32_t st0 = a.status[b];
-    a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
-    if (BOX && a.qp_stats) {
-      a.qp_stats[2 * b] = n_fwd;
-      a.qp_stats[2 * b + 1] = n_bst;
-    }
-  }
+  if constexpr (!BOX) finish();   // (the box kernel finishes each instance as it converges)
 }
 
 }  // namespace asq
@@ -690,8 +727,20 @@ template <class T>
 __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false>(a); }
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
-  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+  unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
+  if (a.as_queue) {   // as many waves as stay resident; the rest of the chunk comes off the counter
+    static const unsigned resident = [] {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      return (unsigned)cus * 4u * (sizeof(T) == 4 ? (unsigned)MPCB_AS_WAVES : 1u);
+    }();
+    if (g > resident) g = resident;
+    const hipError_t e = hipMemsetAsync(a.as_queue, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+  }
   const bool w32 = a.N <= 32;   // (the stage masks fit 32 bits)
   if constexpr (sizeof(T) == 4) {
     if (w32) hipLaunchKernelGGL(as_kernel_f32<true>, dim3(g), dim3(64), lds, st, a);

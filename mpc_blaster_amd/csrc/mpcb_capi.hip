@@ -290,7 +290,8 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     return fail(MPCB_E_HIP, "weights upload: %s", hipGetErrorString(e));
   }
   if (cfg->box_u && (full || h->split)) {
-    e = hipMalloc((void**)&h->qp_stats, (size_t)max_batch * 2 * sizeof(int32_t));
+    // (+ 16: the 12/4 active-set kernel's work counter after the statistics)
+    e = hipMalloc((void**)&h->qp_stats, ((size_t)max_batch * 2 + 16) * sizeof(int32_t));
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
       (void)hipFree(h->weights);
@@ -410,6 +411,9 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH2_REC : nullptr;
       a.qp_stats = h->qp_stats;
+      // the active-set kernel's work counter (MPCB_AS_PERSIST=0: one wave per instance quad)
+      a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
+      if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));
