@@ -97,3 +97,28 @@ def test_config_defaults_equal_reference_json_slice():
     assert abs(c.dt - pin['solver_options']['time_steps'][0]) < 1e-15
     b = MPCConfig(lbu=np.asarray(pin['lbu'][:4]), ubu=np.asarray(pin['ubu'][:4]))
     assert b.to_c().box_u == 1
+
+
+def test_packed_value_function_record_covers_every_entry():
+    """The PS2 record (mpcb_kernels.h): lane j stores P[j][(j + d) % 12] for d = 0..6
+    (mpcb_split.hip riccati_body, the store after the symmetric publish), and the active-set
+    kernel's restart reads P[i][j] from lane i's slot (j - i) % 12 when that is <= 6, else from
+    lane j's slot (i - j) % 12 (mpcb_as.hip).  Restated here on a random symmetric P: the read
+    rule recovers all 144 entries from the 12 x 7 stored slots."""
+    hdr = open(os.path.join(REPO, 'mpc_blaster_amd', 'csrc', 'mpcb_kernels.h')).read()
+    ps2_w = int(re.search(r'PS2_W\s*=\s*(\d+)', hdr).group(1))
+    nx = 12
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal((nx, nx))
+    P = a + a.T
+    rec = np.full((nx, ps2_w), np.nan)
+    for j in range(nx):
+        for d in range(7):
+            o = (j + d) % nx
+            rec[j, d] = P[max(o, j), min(o, j)]   # the lower triangle the kernel reads
+    assert not np.isnan(rec[:, :7]).any() and ps2_w >= 8   # slot 7 holds p_k[j]
+    for jx in range(nx):        # reader lane jx rebuilds column jx: Pc[i] = P[i][jx]
+        for i in range(nx):
+            dd = (jx - i) % nx
+            v = rec[i, dd] if dd <= 6 else rec[jx, nx - dd]
+            assert v == P[i, jx]

@@ -333,6 +333,53 @@ def test_full_size_c4_box_properties():
     assert relerr(u1.cpu().numpy(), u0[:512].cpu().numpy()).max() < 5e-5
 
 
+@pytest.mark.parametrize('dtype', ['f32', 'f64'])
+def test_box_work_counter_grid_is_bit_identical(dtype):
+    """The active-set kernel's resident grid (a group whose instance converged takes the next one
+    from a per-chunk work counter, mpcb_as.hip) computes each instance with the same arithmetic as
+    one wave per quad (MPCB_AS_PERSIST=0): U, X and status are bit-identical, over several chunks
+    (MPCB_CHUNK=1024: the counter is reset per chunk) with a ragged last chunk and quad, and a
+    sampled slice (plus every instance with a non-zero status) matches the oracle."""
+    B, N = 3001, 20
+    old = os.environ.get('MPCB_CHUNK')
+    os.environ['MPCB_CHUNK'] = '1024'
+    try:
+        m = _mpc(N, dtype, box=True, max_batch=B)
+    finally:
+        if old is None:
+            os.environ.pop('MPCB_CHUNK')
+        else:
+            os.environ['MPCB_CHUNK'] = old
+    assert m.path == 'split'
+    d = m.gen_inputs(B, seed=2024, ref='hover')
+    res = []
+    for persist in ('1', '0'):
+        os.environ['MPCB_AS_PERSIST'] = persist
+        try:
+            u0 = m.solve(d['x0'], d['xref'], d['uref'], want_traj=True).clone()
+        finally:
+            os.environ.pop('MPCB_AS_PERSIST')
+        res.append((u0, m.get_input_trajectory().clone(), m.get_state_trajectory().clone(),
+                    m.get_status().clone()))
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    st = res[0][3].cpu().numpy()
+    bad = np.nonzero(st)[0]
+    assert len(bad) <= 2 and (st[bad] == 2).all()   # MPCB_STATUS_MAXITER
+    idx = np.unique(np.concatenate([[0, 1, 1023, 1024, 2047, 2048, 3000], bad]))
+    x0 = d['x0'][idx].double().cpu().numpy()
+    xr = np.broadcast_to(d['xref'][0].double().cpu().numpy(), (len(idx), N + 1, 12)).copy()
+    ur = np.broadcast_to(d['uref'][0].double().cpu().numpy(), (len(idx), N, 4)).copy()
+    o = mpc_solve(x0, xr, ur, _spec(N, box=True))
+    tol = 5e-5 if dtype == 'f32' else 1e-9
+    # (the oracle's active-set loop also stops at max_iter on the instances the device flags; their
+    # last iterates are not a KKT point and are compared only by status)
+    assert (o['status'] == st[idx]).all()
+    ok = o['status'] == 0
+    assert ok.sum() >= 7 and relerr(res[0][1][idx].cpu().numpy(), o['U'])[ok].max() < tol
+
+
 def test_closed_loop_matches_oracle_fp64():
     """Receding-horizon loop (simulation_blaster.py:56-107) with the persistent SQP_RTI iterate."""
     from mpc_blaster_amd.closed_loop import closed_loop
