@@ -185,13 +185,26 @@ __device__ __forceinline__ int row_or(int v) {
   return f > 0.f ? 1 : 0;
 }
 
-// per-instance LDS block
+// per-instance LDS block.  Bank layout (MI355X_MICROARCH.md §LDS: ds_read_b64 banks (a/4) mod 64
+// over 32-lane halves = two instances; ds_write_b64 banks (a/4) mod 32 over 16-lane groups):
+//  - the block is 32 dwords mod 64 long (fp64; 16 mod 32 in fp32), so the two instances of a half
+//    read opposite halves of the bank row;
+//  - X's columns are stored at xpos(s): the 16 columns the exchange reads are contiguous (32
+//    dwords), state 8's (never read back) last -- stored by s they spanned 34 dwords and wrapped
+//    onto the sibling instance's banks;
+//  - HU rows are 9 long: the six input lanes' stores of one entry hit distinct bank pairs (rows of
+//    8 put lanes m and m + 2 on one bank, 3-way);
+//  - V and the rows of s Q hold the states at xpos too (by s, lanes s = 0 and 16 shared a bank:
+//    the compiler pairs the Q reads as ds_read2_b64, banked (a/4) mod 32).
+__host__ __device__ constexpr int xpos(int s) { return s < OM ? s : s == OM ? NX17 - 1 : s - 1; }
 template <class T> struct Lds {
-  T V[24];            // cost residual (ybar + iterate - yref) by z index
-  T HU[NU17][8];      // input lane m: G[17+n, 17+m] (n < 6), h_u[m], G[8, 17+m]
+  T V[24];            // cost residual (ybar + iterate - yref): state i at xpos(i), input n at 17 + n
+  T HU[NU17][9];      // input lane m: G[17+n, 17+m] (n < 6), h_u[m], G[8, 17+m]
   T YC[6][17];        // lane t: Y[c, z(t)] for the identity states c = ids(0..5) (stride 17: banks)
-  T X[LN][NX17];      // P_new columns (symmetric exchange)
+  T X[LN][NX17];      // P_new columns (symmetric exchange), entry i of lane t's column at xpos(i)
+  T pad[12];
 };
+static_assert(sizeof(Lds<double>) / 4 % 64 == 32 && sizeof(Lds<float>) / 4 % 32 == 16, "Lds bank layout");
 
 template <class T>
 struct Ctx {
@@ -201,7 +214,7 @@ struct Ctx {
   const T* xr;
   const T* ur;
   Lds<T>& L;
-  const T* sQ;        // s * Q (row-major 17 x 17), LDS
+  const T* sQ;        // s * Q (row-major 17 x 17, Q[i][j] at i * 17 + xpos(j): banks), LDS
   const T* sR;        // s * R (6 x 6), LDS
   int t, s, z, m;     // lane in the row, owned state, z column, input index (input lanes; else 0)
   bool in, valid;
@@ -325,14 +338,14 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       xs += ys;
       x8 += y8;
     }
-    L.V[s] = xs - r.xr[(int64_t)Nq * NX17 + s];
-    L.V[OM] = x8 - r.xr[(int64_t)Nq * NX17 + OM];
+    L.V[xpos(s)] = xs - r.xr[(int64_t)Nq * NX17 + s];
+    L.V[xpos(OM)] = x8 - r.xr[(int64_t)Nq * NX17 + OM];
     wave_lds_sync();
     pj = T(0);
     p8 = T(0);
 #pragma unroll
     for (int i = 0; i < NX17; ++i) {
-      const T vi = L.V[i];
+      const T vi = L.V[xpos(i)];
       pj += W.QN[s * NX17 + i] * vi;
       p8 += W.QN[OM * NX17 + i] * vi;
       Pc[i] = W.QN[i * NX17 + s];
@@ -398,8 +411,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       r.w.DX[(int64_t)kq * NX17 + OM] = ic.dx8;
     }
     // cost residual (ybar [+ iterate] - yref) into LDS (general Q, R)
-    L.V[s] = (ipm ? cu.xs + ic.dxs : cu.xs) - cu.xrs;
-    L.V[OM] = (ipm ? cu.x8 + ic.dx8 : cu.x8) - cu.xr8;
+    L.V[xpos(s)] = (ipm ? cu.xs + ic.dxs : cu.xs) - cu.xrs;
+    L.V[xpos(OM)] = (ipm ? cu.x8 + ic.dx8 : cu.x8) - cu.xr8;
     if (in) L.V[NX17 + r.m] = (ipm ? cu.ub + ic.du : cu.ub) - cu.urm;
     // identity rows of this lane's Y for the identity-state lanes (their G column, by symmetry)
 #pragma unroll
@@ -459,10 +472,10 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
     T gs = T(0);            // (MEH) the state's gradient without the p term
 #pragma unroll
     for (int i = 0; i < NX17; ++i) {
-      const T wq = r.sQ[i * NX17 + s];
+      const T wq = r.sQ[i * NX17 + xpos(s)];
       Gs[i] += wq;
-      if constexpr (MEH) gs += wq * L.V[i];
-      else hs += wq * L.V[i];
+      if constexpr (MEH) gs += wq * L.V[xpos(i)];
+      else hs += wq * L.V[xpos(i)];
     }
     if constexpr (MEH) hs = hs + gs;
     // row 8 of every lane's G column is needed as the distributed column 8 of G; G[8,8] itself:
@@ -483,8 +496,8 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
       T gr8 = T(0);
 #pragma unroll
       for (int i = 0; i < NX17; ++i) {
-        if constexpr (MEH) gr8 += r.sQ[OM * NX17 + i] * L.V[i];
-        else h8 += r.sQ[OM * NX17 + i] * L.V[i];
+        if constexpr (MEH) gr8 += r.sQ[OM * NX17 + xpos(i)] * L.V[xpos(i)];
+        else h8 += r.sQ[OM * NX17 + xpos(i)] * L.V[xpos(i)];
       }
       if constexpr (MEH) {   // (no state rows in the Mehrotra kernel: the gradients are complete)
         h8 = h8 + gr8;
@@ -493,7 +506,7 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
         gv[OM] = gr8;
         gv[in ? NX17 + r.m : 23] = gu_own;
       }
-      G88 += r.sQ[OM * NX17 + OM];
+      G88 += r.sQ[OM * NX17 + xpos(OM)];
     }
     if (sbox && k > 0) {   // state-box rows of this stage: barrier terms on the state diagonals
       T D, d;
@@ -589,14 +602,14 @@ __device__ __forceinline__ bool backward(const Ctx<T>& r, T smu, T apend = T(0),
 #endif
     // symmetric by construction: entry (i, s) from the lane max(own, owner of i)
 #pragma unroll
-    for (int i = 0; i < NX17; ++i) L.X[t][i] = Pn[i];
+    for (int i = 0; i < NX17; ++i) L.X[t][xpos(i)] = Pn[i];
     wave_lds_sync();
 #pragma unroll
     for (int i = 0; i < NX17; ++i) {
       if (i == OM) {
         Pc[i] = Pn[i];
       } else {
-        const T o = L.X[tstate(i)][s];
+        const T o = L.X[tstate(i)][xpos(s)];
         Pc[i] = csel(lane_mask(tstate(i) > t), o, Pn[i]);
       }
     }
@@ -871,7 +884,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
   const bool in = t >= 8 && t < 14;
   const int s = sown(t);
   const int m = in ? t - 8 : 0;
-  for (int e = lane; e < NX17 * NX17; e += 64) sQ[e] = a.s * W.Q[e];
+  for (int e = lane; e < NX17 * NX17; e += 64) sQ[e / NX17 * NX17 + xpos(e % NX17)] = a.s * W.Q[e];
   for (int e = lane; e < NU17 * NU17; e += 64) sR[e] = a.s * W.R[e];
   __syncthreads();
   Ctx<T> r{a, Ws17<T>(a.ws + c * full17_elems(N), N), WsM17<T>(Ws17<T>(a.ws + c * full17_elems(N), N), N), a.xref + b * a.xref_sb, a.uref + b * a.uref_sb,
