@@ -321,7 +321,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       T ncol[NX], ne, nyb, ngp = T(0);
       auto bload = [&](int k) {
         if (tv >= 0) {
+#if MPCB_AS_AB2
           ldv<T, NX>(AB.at(k) + tv * NX, ncol);
+#else
+          const T* rows = ABT.at(k) + tv;   // column tv of the stage's ABT2 rows
+#pragma unroll
+          for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
+#endif
         } else {   // position / velocity directions: e_j, e_j + h e_{j-6}
 #pragma unroll
           for (int i = 0; i < NX; ++i) ncol[i] = (i == j ? T(1) : T(0)) + ((j >= 6 && i == j - 6) ? h : T(0));

@@ -406,7 +406,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
       a.imajor = h->cfg.box_u ? 0 : 1;
       if (const char* e = getenv("MPCB_RM_IMAJOR")) a.imajor = atoi(e) != 0;
-      a.AB = (h->cfg.box_u || h->small) ? ab : nullptr;
+      a.AB = ((h->cfg.box_u && MPCB_AS_AB2) || h->small) ? ab : nullptr;
       a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH2_REC : nullptr;

@@ -86,6 +86,12 @@ constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 //                  in slot 7 (84 slots for its 78 distinct entries); written by P2's unconstrained
 //                  pass and by every stage the active-set kernel recomputes (its restart points)
 constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
+// The active-set kernel's backward reads its [A|B] column out of the ABT2 rows (12 strided loads:
+// the masked backward recomputes ~2/3 of the stage-instances once, the forward passes read the
+// rows ~4 times), so P2 writes [A|B] once; MPCB_AS_AB2=1 restores the separate AB2 column export.
+#ifndef MPCB_AS_AB2
+#define MPCB_AS_AB2 0
+#endif
 constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, GH2_REC = 4 * 20,
               PS2_REC = 12 * PS2_W;
 
