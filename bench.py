@@ -238,7 +238,8 @@ def phase_kernels(w):
     names = {'nominal': f'nominal_quad_kernel<{t}>' if small else f'nominal_kernel<{t}>',
              'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}>'}
     if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
-        names['forward'] = f'as_kernel_{w["dtype"]}'
+        # (as_kernel_*<true>: the 32-bit stage masks of N <= 32, mpcb_as.hip launch_as)
+        names['forward'] = f'as_kernel_{w["dtype"]}<{"true" if w["N"] <= 32 else "false"}>'
     elif not w['hist']:   # small chunks: the DPP forward pass over P2's row-major exports
         names['forward'] = f'fwd_rm_kernel<{t}>' if small else f'forward_kernel<{t}, false>'
     return names
