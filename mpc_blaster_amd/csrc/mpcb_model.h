@@ -29,19 +29,40 @@ struct Model {
 // path that costs ~4x the instructions and registers on every call; here it is only the
 // (never taken in practice) fallback.  Three calls per f evaluation make this the dominant
 // cost of the nominal passes.
+// Horner step t * z + c as a three-address v_fma_f64 (MPCB_SC_ASM, default on).  Left to itself the
+// compiler turns each step into v_fmac_f64 (the addend is the destination) and so copies the
+// loop-invariant coefficient first: one v_mov per step, ~14 per call, 56 per RK4 interval of the
+// issue-bound P1 rollout.
+#ifndef MPCB_SC_ASM
+#define MPCB_SC_ASM 1
+#endif
+__device__ __forceinline__ double hstep(double t, double z, double c) {
+#if MPCB_SC_ASM
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(t), "v"(z), "v"(c));
+  return r;
+#else
+  return fma(t, z, c);
+#endif
+}
 __device__ __forceinline__ void sc(double a, double* s, double* c) {
   if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
   const double n = rint(a * 6.36619772367581382433e-01);           // 2/pi
   double r = fma(-n, 1.57079632673412561417e+00, a);              // pio2_1 (33 bits)
   r = fma(-n, 6.07710050650619224932e-11, r);                     // pio2_1t
   const double z = r * r;
-  const double ps = -1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 +
-                    z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
-                    z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10))));
+  double ps = hstep(1.58969099521155010221e-10, z, -2.50507602534068634195e-08);
+  ps = hstep(ps, z, 2.75573137070700676789e-06);
+  ps = hstep(ps, z, -1.98412698298579493134e-04);
+  ps = hstep(ps, z, 8.33333333332248946124e-03);
+  ps = hstep(ps, z, -1.66666666666666324348e-01);
   const double sr = fma(r * z, ps, r);
-  const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
-                    z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
-                    z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  double pc = hstep(-1.13596475577881948265e-11, z, 2.08757232129817482790e-09);
+  pc = hstep(pc, z, -2.75573143513906633035e-07);
+  pc = hstep(pc, z, 2.48015872894767294178e-05);
+  pc = hstep(pc, z, -1.38888888888741095749e-03);
+  pc = hstep(pc, z, 4.16666666666666019037e-02);
+  pc = z * pc;
   const double hz = 0.5 * z;
   const double w = 1.0 - hz;
   const double cr = w + (((1.0 - w) - hz) + z * pc);
