@@ -45,23 +45,55 @@ __device__ __forceinline__ double hstep(double t, double z, double c) {
   return fma(t, z, c);
 #endif
 }
-__device__ __forceinline__ void sc(double a, double* s, double* c) {
+// sin/cos polynomial coefficients (fdlibm __kernel_sin / __kernel_cos), highest degree first
+struct ScConst {
+  __device__ static constexpr double s(int i) {
+    constexpr double t[6] = {1.58969099521155010221e-10, -2.50507602534068634195e-08,
+                             2.75573137070700676789e-06, -1.98412698298579493134e-04,
+                             8.33333333332248946124e-03, -1.66666666666666324348e-01};
+    return t[i];
+  }
+  __device__ static constexpr double c(int i) {
+    constexpr double t[6] = {-1.13596475577881948265e-11, 2.08757232129817482790e-09,
+                             -2.75573143513906633035e-07, 2.48015872894767294178e-05,
+                             -1.38888888888741095749e-03, 4.16666666666666019037e-02};
+    return t[i];
+  }
+};
+// The same coefficients as loop-invariant registers the compiler cannot see into: used by the
+// serial P1 rollout, where the compiler otherwise re-assembles some constant pairs from copied
+// halves at every call (7 v_mov_b32 per sin/cos).  Identical values, identical results.
+struct ScRegs {
+  double vs[6], vc[6];
+  __device__ __forceinline__ ScRegs() {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      vs[i] = ScConst::s(i); vc[i] = ScConst::c(i);
+      asm volatile("" : "+v"(vs[i]));
+      asm volatile("" : "+v"(vc[i]));
+    }
+  }
+  __device__ __forceinline__ double s(int i) const { return vs[i]; }
+  __device__ __forceinline__ double c(int i) const { return vc[i]; }
+};
+template <class K>
+__device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
   if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
   const double n = rint(a * 6.36619772367581382433e-01);           // 2/pi
   double r = fma(-n, 1.57079632673412561417e+00, a);              // pio2_1 (33 bits)
   r = fma(-n, 6.07710050650619224932e-11, r);                     // pio2_1t
   const double z = r * r;
-  double ps = hstep(1.58969099521155010221e-10, z, -2.50507602534068634195e-08);
-  ps = hstep(ps, z, 2.75573137070700676789e-06);
-  ps = hstep(ps, z, -1.98412698298579493134e-04);
-  ps = hstep(ps, z, 8.33333333332248946124e-03);
-  ps = hstep(ps, z, -1.66666666666666324348e-01);
+  double ps = hstep(k.s(0), z, k.s(1));
+  ps = hstep(ps, z, k.s(2));
+  ps = hstep(ps, z, k.s(3));
+  ps = hstep(ps, z, k.s(4));
+  ps = hstep(ps, z, k.s(5));
   const double sr = fma(r * z, ps, r);
-  double pc = hstep(-1.13596475577881948265e-11, z, 2.08757232129817482790e-09);
-  pc = hstep(pc, z, -2.75573143513906633035e-07);
-  pc = hstep(pc, z, 2.48015872894767294178e-05);
-  pc = hstep(pc, z, -1.38888888888741095749e-03);
-  pc = hstep(pc, z, 4.16666666666666019037e-02);
+  double pc = hstep(k.c(0), z, k.c(1));
+  pc = hstep(pc, z, k.c(2));
+  pc = hstep(pc, z, k.c(3));
+  pc = hstep(pc, z, k.c(4));
+  pc = hstep(pc, z, k.c(5));
   pc = z * pc;
   const double hz = 0.5 * z;
   const double w = 1.0 - hz;
@@ -71,6 +103,7 @@ __device__ __forceinline__ void sc(double a, double* s, double* c) {
   *s = (q & 2) ? -s0 : s0;
   *c = ((q + 1) & 2) ? -c0 : c0;
 }
+__device__ __forceinline__ void sc(double a, double* s, double* c) { sc(a, s, c, ScConst{}); }
 __device__ __forceinline__ void sc(float a, float* s, float* c) {
   if (!(fabsf(a) < 8192.0f)) { sincosf(a, s, c); return; }
   const float n = rintf(a * 0.636619772367581343f);

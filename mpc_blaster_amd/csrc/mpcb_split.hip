@@ -249,8 +249,79 @@ struct TrigQuad {
   }
 };
 
-constexpr int QI = WAVE / 4;   // instances per workgroup of the quad rollout
+// The angle a quad lane takes the sin/cos of, carried through the RK4 stages by the lane itself:
+// its rate is f[3 + g] = wx + tt·a, b or ict·a (mpcb_model.h f_nom_lin), i.e.
+// (β0·tt + β2·ict)·a + α·wx + γ·b with per-lane 0/1 coefficients, so every stage's angle costs
+// three FMAs and no lane select (the select rebuilt its lane masks from spilled SGPRs at every
+// f evaluation).  The products by 0 and 1 are exact: the angles equal those of the plain stage
+// update x + h·k bit for bit.
+template <class T> struct ScFor { using type = ScConst; };   // fp32: sc(float) has its own
+template <> struct ScFor<double> { using type = ScRegs; };
 template <class T>
+struct TrigOwn {
+  const T* ang;
+  const typename ScFor<T>::type* k;
+  __device__ __forceinline__ void operator()(const T* __restrict__, T& sf, T& cf, T& st, T& ct,
+                                             T& sp, T& cp) const {
+    T s, c;
+    if constexpr (sizeof(T) == 8) sc(*ang, &s, &c, *k);
+    else sc(*ang, &s, &c);
+    sf = qbcast<0>(s); cf = qbcast<0>(c);
+    st = qbcast<1>(s); ct = qbcast<1>(c);
+    sp = qbcast<2>(s); cp = qbcast<2>(c);
+  }
+};
+template <class T>
+struct AngRate {
+  T al, ga, b0, b2;
+  __device__ __forceinline__ explicit AngRate(int g)
+      : al(T(g == 0)), ga(T(g == 1)), b0(T(g == 0)), b2(T(g >= 2)) {}
+  // rate of the lane's angle from the stage's captured scalars (c[6] = ict, c[7] = tt, c[8] = a,
+  // c[17] = wx) and f[4] = b
+  __device__ __forceinline__ T operator()(const T* c, T b) const {
+    return fma(fma(b0, c[7], b2 * c[6]), c[8], fma(al, c[17], ga * b));
+  }
+};
+// rk4_nom (mpcb_model.h) with the lane's angle ``ang`` (= x[3 + g] on entry) carried separately
+template <class T, class Sink>
+__device__ __forceinline__ void rk4_nom_own(const T* __restrict__ x, T ang, const T* __restrict__ u,
+                                            T h, const Model<T>& M, const T w[3],
+                                            T* __restrict__ xn, const AngRate<T>& rate,
+                                            const typename ScFor<T>::type& kc, Sink&& sink) {
+  constexpr int NX = 12;
+  T k[NX], xs[NX], c[LIN_N];
+  const T h2 = T(0.5) * h, h6 = h / T(6);
+  T a_s = ang;
+  const TrigOwn<T> trig{&a_s, &kc};
+  f_nom_lin<T>(x, u, M, w, k, c, trig);
+  sink(0, c);
+  a_s = fma(h2, rate(c, k[4]), ang);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] = k[i]; if (i < 3 || i > 5) xs[i] = x[i] + h2 * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
+  sink(1, c);
+  a_s = fma(h2, rate(c, k[4]), ang);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; if (i < 3 || i > 5) xs[i] = x[i] + h2 * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
+  sink(2, c);
+  a_s = fma(h, rate(c, k[4]), ang);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { xn[i] += T(2) * k[i]; if (i < 3 || i > 5) xs[i] = x[i] + h * k[i]; }
+  f_nom_lin<T>(xs, u, M, w, k, c, trig);
+  sink(3, c);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xn[i] = x[i] + h6 * (xn[i] + k[i]);
+}
+
+#ifndef MPCB_P1_OWNANG
+#define MPCB_P1_OWNANG 1   // each quad lane carries its own angle (TrigOwn / AngRate)
+#endif
+constexpr int QI = WAVE / 4;   // instances per workgroup of the quad rollout
+// ITER: iterate mode (a.mode == MPCB_MODE_ITERATE) as a template argument, so that each
+// instantiation's stage loop has one shape (no loop-carried select between the rolled-out and the
+// loaded state, no mode branches or their exec masks on the serial chain)
+template <class T, bool ITER>
 __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
   constexpr int NQ = QI / SS;
   __shared__ __attribute__((aligned(16))) T lds_cc[QuadStore<T, CCS_REC, NQ>::ELEMS];
@@ -269,14 +340,19 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
   const int nqv = (int)((nq - c0 / SS) < NQ ? nq - c0 / SS : NQ);
   const int64_t b = a.b0 + c;
   const int N = a.N;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  constexpr bool iterate = ITER;
 #if MPCB_P1_ALLW
   // every lane of the quad stages the (identical) values: no exec-masked branches on the chain
   const bool lead = true;
 #else
   const bool lead = g == 0;                        // the lane that stages the quad's values
 #endif
+#if MPCB_P1_OWNANG
+  const AngRate<T> rate(g);
+  const typename ScFor<T>::type kc;   // once, outside the stage loop
+#else
   const TrigQuad trig{g};
+#endif
   T w[3] = {T(0), T(0), T(0)};
   if (a.wind) {
     w[0] = a.wind[b * a.wind_sb]; w[1] = a.wind[b * a.wind_sb + 1]; w[2] = a.wind[b * a.wind_sb + 2];
@@ -312,12 +388,20 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
       for (int m = 0; m < NU; ++m) xus.put(ci, NX + m, u[m]);
     }
     T xn[NX];
+#if MPCB_P1_OWNANG
+    rk4_nom_own<T>(x, sel<3>(x + 3, g), u, a.h, a.M, w, xn, rate, kc, [&](int stage, const T* cv) {
+#else
     rk4_nom<T>(x, u, a.h, a.M, w, xn, [&](int stage, const T* cv) {
+#endif
       if (lead) {
 #pragma unroll
         for (int i = 0; i < LIN_N; ++i) ccs.put(ci, stage * LIN_N + i, cv[i]);
       }
+#if MPCB_P1_OWNANG
+    });
+#else
     }, trig);
+#endif
     STAMP(14);
     if (iterate) {
       const T* nx = xbp + (int64_t)(k + 1) * NX;
@@ -855,8 +939,8 @@ template <class T> int64_t split_elems_per_instance(int N, int iterate, int box)
 
 template <class T>
 __global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_wave<T>(a); }
-template <class T>
-__global__ void __launch_bounds__(64) nominal_quad_kernel(SplitArgs<T> a) { nominal_quad<T>(a); }
+template <class T, bool ITER>
+__global__ void __launch_bounds__(64) nominal_quad_kernel(SplitArgs<T> a) { nominal_quad<T, ITER>(a); }
 template <class T, bool USE_CC>
 __global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
@@ -886,8 +970,11 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (a.quad_p1)
-    hipLaunchKernelGGL((nominal_quad_kernel<T>), dim3((unsigned)((a.nb + QI - 1) / QI)), dim3(WAVE), 0, st, a);
+  if (a.quad_p1) {
+    const dim3 gq((unsigned)((a.nb + QI - 1) / QI));
+    if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((nominal_quad_kernel<T, true>), gq, dim3(WAVE), 0, st, a);
+    else hipLaunchKernelGGL((nominal_quad_kernel<T, false>), gq, dim3(WAVE), 0, st, a);
+  }
   else
     hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);

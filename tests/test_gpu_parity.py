@@ -173,6 +173,45 @@ def test_sim_step_and_histogram():
     assert np.array_equal(counts, ref)
 
 
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_wrapped_euler_angles_quad_rollout_fp64(mode):
+    """The quad-lane rollout (split path, chunks <= 16384) carries each lane's Euler angle through
+    the RK4 stages itself (mpcb_split.hip rk4_nom_own).  Angles offset by 2*pi*k, up to past 2^19
+    rad where sin/cos leave the Cody-Waite range for the ocml fallback on that lane only, with the
+    reference offset alike, must still match the oracle.  Tolerance: the stage angle x + h/2*k is
+    rounded at |x| ~ 6e5 to ~1.2e-10 absolute (the device contracts it into one fma, NumPy rounds
+    twice), which moves sin/cos by that much; 1e-9 elsewhere."""
+    N, B = 12, 24
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    k = np.array([0, 1, -3, 1e3, -1e4, 1e5, 9e4, 83500.0] * 3)[:B]   # 2*pi*83500 > 2^19
+    off = np.zeros((B, 12))
+    off[:, 3] = 2 * np.pi * np.roll(k, 1)
+    off[:, 4] = 2 * np.pi * np.roll(k, 2)
+    off[:, 5] = 2 * np.pi * k
+    x0 = inp['x0'] + off
+    xref = inp['xref'] + off[:, None, :]
+    m = _mpc(N, 'f64', max_batch=B, path='split')
+    spec = _spec(N)
+    if mode == 'rollout':
+        m.solve(x0, xref, inp['uref'])
+        o = mpc_solve(x0, xref, inp['uref'], spec)
+    else:
+        rng = np.random.default_rng(3)
+        xbar = xref + rng.normal(scale=0.05, size=xref.shape)
+        ubar = inp['uref'] + rng.normal(scale=1.0, size=inp['uref'].shape)
+        m.solve_iterate(x0, xbar, ubar, xref, inp['uref'])
+        o = mpc_solve(x0, xref, inp['uref'], spec, mode='iterate', xbar=xbar, ubar=ubar)
+    torch.cuda.synchronize()
+    e_u = relerr(m.get_control().cpu().numpy(), o['u0'])
+    e_x = relerr(m.get_state_trajectory().cpu().numpy() - off[:, None, :], o['X'] - off[:, None, :])
+    big = np.abs(off).max(axis=1) > 1e3
+    print(f'{mode}: small offsets u0 {e_u[~big].max():.2e} X {e_x[~big].max():.2e}; '
+          f'large u0 {e_u[big].max():.2e} X {e_x[big].max():.2e}')
+    assert (m.get_status().cpu().numpy() == 0).all()
+    assert e_u[~big].max() < 1e-9 and e_x[~big].max() < 1e-9
+    assert e_u[big].max() < 1e-6 and e_x[big].max() < 1e-6
+
+
 @pytest.mark.parametrize('path', ['fused', 'split', 'small'])
 def test_u0_only_path_equals_full_path(path):
     N, B = 20, 64
