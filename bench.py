@@ -235,7 +235,7 @@ def phase_kernels(w):
     """
     t = 'float' if w['dtype'] == 'f32' else 'double'
     small = w['batch'] <= 16384
-    names = {'nominal': f'nominal_quad_kernel<{t}>' if small else f'nominal_kernel<{t}>',
+    names = {'nominal': f'nominal_quad_kernel<{t}, false>' if small else f'nominal_kernel<{t}>',
              'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}>'}
     if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
         # (as_kernel_*<true>: the 32-bit stage masks of N <= 32, mpcb_as.hip launch_as)
