@@ -235,13 +235,14 @@ def phase_kernels(w):
     """
     t = 'float' if w['dtype'] == 'f32' else 'double'
     small = w['batch'] <= 16384
-    names = {'nominal': f'nominal_quad_kernel<{t}, false>' if small else f'nominal_kernel<{t}>',
-             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}>'}
+    # (the rollout-mode instantiations: the mode is a template argument of P1, P2 and P3)
+    names = {'nominal': f'nominal_quad_kernel<{t}, false>' if small else f'nominal_kernel<{t}, false>',
+             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}, false>'}
     if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
         # (as_kernel_*<true>: the 32-bit stage masks of N <= 32, mpcb_as.hip launch_as)
-        names['forward'] = f'as_kernel_{w["dtype"]}<{"true" if w["N"] <= 32 else "false"}>'
+        names['forward'] = f'as_kernel_{w["dtype"]}<{"true" if w["N"] <= 32 else "false"}, false>'
     elif not w['hist']:   # small chunks: the DPP forward pass over P2's row-major exports
-        names['forward'] = f'fwd_rm_kernel<{t}>' if small else f'forward_kernel<{t}, false>'
+        names['forward'] = f'fwd_rm_kernel<{t}, false>' if small else f'forward_kernel<{t}, false, false>'
     return names
 
 

@@ -37,6 +37,9 @@
 #ifndef MPCB_AS_FDEPTH   // forward-pass prefetch ring (stages): active-set kernel
 #define MPCB_AS_FDEPTH 1
 #endif
+#ifndef MPCB_AS_ITER_T   // the mode as a template argument (as in P1 / P2 / P3)
+#define MPCB_AS_ITER_T 1
+#endif
 #ifndef MPCB_FWD_FDEPTH  // the same for the unconstrained forward pass (fwd_rm_kernel)
 #define MPCB_FWD_FDEPTH 2
 #endif
@@ -168,7 +171,7 @@ template <bool W32> struct Masks {
   __device__ static __forceinline__ int clz(M v) { if constexpr (W32) return __builtin_clz(v); else return __clzll(v); }
 };
 
-template <class T, bool BOX, bool W32 = false>
+template <class T, bool BOX, bool W32 = false, bool ITER = false>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   using Mk = Masks<W32>;
   using M = typename Mk::M;
@@ -187,7 +190,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   const int N = a.N;
   const T h = a.h;
   const Weights<T>& W = *a.W;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const bool iterate = MPCB_AS_ITER_T ? ITER : a.mode == MPCB_MODE_ITERATE;   // (see riccati_body)
   const T lbm = W.lbu[ju], ubm = W.ubu[ju];
   constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
   const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
@@ -724,13 +727,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 
 }  // namespace asq
 
-template <bool W32>
+template <bool W32, bool ITER = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS_WAVES, 8)))
-as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true, W32>(a); }
-template <bool W32>
-__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true, W32>(a); }
-template <class T>
-__global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false>(a); }
+as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true, W32, ITER>(a); }
+template <bool W32, bool ITER = false>
+__global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true, W32, ITER>(a); }
+template <class T, bool ITER = false>
+__global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false, false, ITER>(a); }
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
@@ -748,12 +751,23 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   const bool w32 = a.N <= 32;   // (the stage masks fit 32 bits)
+  const bool it = MPCB_AS_ITER_T && a.mode == MPCB_MODE_ITERATE;
   if constexpr (sizeof(T) == 4) {
-    if (w32) hipLaunchKernelGGL(as_kernel_f32<true>, dim3(g), dim3(64), lds, st, a);
-    else hipLaunchKernelGGL(as_kernel_f32<false>, dim3(g), dim3(64), lds, st, a);
+    if (it) {
+      if (w32) hipLaunchKernelGGL((as_kernel_f32<true, true>), dim3(g), dim3(64), lds, st, a);
+      else hipLaunchKernelGGL((as_kernel_f32<false, true>), dim3(g), dim3(64), lds, st, a);
+    } else {
+      if (w32) hipLaunchKernelGGL(as_kernel_f32<true>, dim3(g), dim3(64), lds, st, a);
+      else hipLaunchKernelGGL(as_kernel_f32<false>, dim3(g), dim3(64), lds, st, a);
+    }
   } else {
-    if (w32) hipLaunchKernelGGL(as_kernel_f64<true>, dim3(g), dim3(64), lds, st, a);
-    else hipLaunchKernelGGL(as_kernel_f64<false>, dim3(g), dim3(64), lds, st, a);
+    if (it) {
+      if (w32) hipLaunchKernelGGL((as_kernel_f64<true, true>), dim3(g), dim3(64), lds, st, a);
+      else hipLaunchKernelGGL((as_kernel_f64<false, true>), dim3(g), dim3(64), lds, st, a);
+    } else {
+      if (w32) hipLaunchKernelGGL(as_kernel_f64<true>, dim3(g), dim3(64), lds, st, a);
+      else hipLaunchKernelGGL(as_kernel_f64<false>, dim3(g), dim3(64), lds, st, a);
+    }
   }
   return hipGetLastError();
 }
@@ -761,7 +775,10 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
 template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
-  hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), lds, st, a);
+  if (MPCB_AS_ITER_T && a.mode == MPCB_MODE_ITERATE)
+    hipLaunchKernelGGL((fwd_rm_kernel<T, true>), dim3(g), dim3(64), lds, st, a);
+  else
+    hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 template hipError_t launch_fwd_rm<double>(const SplitArgs<double>&, hipStream_t);

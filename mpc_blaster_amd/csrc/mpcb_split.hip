@@ -160,7 +160,7 @@ __device__ __forceinline__ void dma_record(unsigned img, const T* src_lane) {
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <class T>
+template <class T, bool ITER>
 __device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
   __shared__ __attribute__((aligned(16))) T lds_cc[QuadStore<T, CCS_REC>::ELEMS];
   __shared__ __attribute__((aligned(16))) T lds_xu[QuadStore<T, XU_REC>::ELEMS];
@@ -177,7 +177,7 @@ __device__ __forceinline__ void nominal_wave(const SplitArgs<T>& a) {
   const int nqv = (int)((nq - c0 / SS) < WQ ? nq - c0 / SS : WQ);
   const int64_t b = a.b0 + c;
   const int N = a.N;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  constexpr bool iterate = ITER;   // (see nominal_quad)
   T w[3] = {T(0), T(0), T(0)};
   if (a.wind) {
     w[0] = a.wind[b * a.wind_sb]; w[1] = a.wind[b * a.wind_sb + 1]; w[2] = a.wind[b * a.wind_sb + 2];
@@ -435,7 +435,17 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
 // EXPORT: code for storing column j of [A|B] (a.AB, a.ABT) and the input rows of the stage
 // Hessian (a.GH) for the 16-lane forward / active-set kernels; each store runs only when its
 // array is set (a separate export-free fp32 instantiation keeps the plain pass's registers lean)
-template <class T, bool EXPORT>
+// ITER: iterate mode as a template argument (MPCB_P2_ITER_T, default on): the rollout-mode
+// instantiation carries no gap pointer, gap prefetch or P·gap term, which frees scalar registers
+// (the fp64 body spills SGPRs to VGPR lanes).  MPCB_P2_ITER_T=0: one instantiation, mode tested
+// at run time as before.
+#ifndef MPCB_P2_ITER_T
+#define MPCB_P2_ITER_T 1
+#endif
+#ifndef MPCB_P2_MVGPR
+#define MPCB_P2_MVGPR 1
+#endif
+template <class T, bool EXPORT, bool ITER = false>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
@@ -447,7 +457,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   const int N = a.N;
   const T s = a.s;
   const Weights<T>& W = *a.W;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  const bool iterate = MPCB_P2_ITER_T ? ITER : a.mode == MPCB_MODE_ITERATE;
   const bool valid = c_raw < a.nb;
   const int64_t c = valid ? c_raw : a.nb - 1;
   const int64_t b = a.b0 + c;
@@ -455,6 +465,15 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   const T* xr = a.xref + b * a.xref_sb;
   const T* ur = a.uref + b * a.uref_sb;
   const T hv = (a.h / T(6)) * T(6);   // the RK4 tangent's position entry of a velocity column
+  // fp64: the model constants of the tangent (J, Jinv, arm lengths, 1/m) as opaque loop-invariant
+  // VGPR pairs instead of kernel-argument SGPR pairs (MPCB_P2_MVGPR, default on): 44 SGPRs the
+  // body otherwise spills to VGPR lanes and reads back at every stage
+  Model<T> Mv = a.M;
+  if constexpr (sizeof(T) == 8 && MPCB_P2_MVGPR) {
+    asm volatile("" : "+v"(Mv.minv), "+v"(Mv.lx), "+v"(Mv.ly), "+v"(Mv.c));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(Mv.J[i]), "+v"(Mv.Jinv[i]));
+  }
 
   // s * blkdiag(Q, R) in LDS: lane j reads column j (= row j), so the stage-cost terms are the
   // same instruction stream in state and input lanes (no divergent branch per stage)
@@ -524,7 +543,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
 #pragma unroll
       for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
-      rk4_tan<T>(cc, dx, du, a.h, a.M, col);
+      rk4_tan<T>(cc, dx, du, a.h, Mv, col);
       STAMP(1);
       const int tv = var_index(j);   // exported: the state-dependent columns only
       if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
@@ -771,7 +790,7 @@ struct FwdLds {
 // USE_CC: integrate the forward tangent from the captured linearisation scalars (small chunks:
 // CC is cache resident) instead of re-evaluating f with sin/cos (large chunks: saves streaming
 // 80 scalars per stage back from HBM).
-template <class T, bool USE_CC>
+template <class T, bool USE_CC, bool ITER>
 __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
   using L = FwdLds<T, USE_CC>;
   constexpr int S = L::S, V = L::V, ROW = L::ROW;
@@ -789,7 +808,7 @@ __device__ __forceinline__ void forward_wave(const SplitArgs<T>& a) {
   const int nvalid = (int)((nb - c0) < WAVE ? nb - c0 : WAVE);
   const int64_t b = a.b0 + c;
   const int N = a.N;
-  const bool iterate = a.mode == MPCB_MODE_ITERATE;
+  constexpr bool iterate = ITER;   // (see nominal_quad)
   T w[3] = {T(0), T(0), T(0)};
   if (a.wind) {
     w[0] = a.wind[b * a.wind_sb]; w[1] = a.wind[b * a.wind_sb + 1]; w[2] = a.wind[b * a.wind_sb + 2];
@@ -937,33 +956,38 @@ template <class T> int64_t split_elems_per_instance(int N, int iterate, int box)
                    : box == 1 ? (int64_t)N * (AB_REC + ABT2_REC) : 0);
 }
 
-template <class T>
-__global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_wave<T>(a); }
+template <class T, bool ITER>
+__global__ void __launch_bounds__(64) nominal_kernel(SplitArgs<T> a) { nominal_wave<T, ITER>(a); }
 template <class T, bool ITER>
 __global__ void __launch_bounds__(64) nominal_quad_kernel(SplitArgs<T> a) { nominal_quad<T, ITER>(a); }
-template <class T, bool USE_CC>
-__global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC>(a); }
+template <class T, bool USE_CC, bool ITER>
+__global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC, ITER>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
-template <bool EXPORT>
+template <bool EXPORT, bool ITER = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_P2_WAVES_F32, 8)))
 riccati_kernel_f32(SplitArgs<float> a) {
-  riccati_body<float, EXPORT>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  riccati_body<float, EXPORT, ITER>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
-template <bool EXPORT>
+template <bool EXPORT, bool ITER = false>
 __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs<double> a) {
-  riccati_body<double, EXPORT>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  riccati_body<double, EXPORT, ITER>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
-template <class T, bool USE_CC>
-static hipError_t launch_forward(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
+template <class T, bool USE_CC, bool ITER>
+static hipError_t launch_forward_m(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
   constexpr size_t bytes = FwdLds<T, USE_CC>::BYTES;
   static_assert(bytes <= 160 * 1024, "P3 LDS carve exceeds the CU's 160 KiB");
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&forward_kernel<T, USE_CC>),
+      reinterpret_cast<const void*>(&forward_kernel<T, USE_CC, ITER>),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((forward_kernel<T, USE_CC>), dim3(grid), dim3(WAVE), bytes, st, a);
+  hipLaunchKernelGGL((forward_kernel<T, USE_CC, ITER>), dim3(grid), dim3(WAVE), bytes, st, a);
   return hipSuccess;
+}
+template <class T, bool USE_CC>
+static hipError_t launch_forward(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
+  return a.mode == MPCB_MODE_ITERATE ? launch_forward_m<T, USE_CC, true>(a, grid, st)
+                                     : launch_forward_m<T, USE_CC, false>(a, grid, st);
 }
 
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
@@ -975,8 +999,10 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((nominal_quad_kernel<T, true>), gq, dim3(WAVE), 0, st, a);
     else hipLaunchKernelGGL((nominal_quad_kernel<T, false>), gq, dim3(WAVE), 0, st, a);
   }
+  else if (a.mode == MPCB_MODE_ITERATE)
+    hipLaunchKernelGGL((nominal_kernel<T, true>), dim3(gw), dim3(WAVE), 0, st, a);
   else
-    hipLaunchKernelGGL((nominal_kernel<T>), dim3(gw), dim3(WAVE), 0, st, a);
+    hipLaunchKernelGGL((nominal_kernel<T, false>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (a.small) {   // linearisation + Riccati + forward over the cached [A|B] (mpcb_box.hip)
     hipError_t e = launch_small<T>(a, st);
@@ -985,12 +1011,20 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     return e != hipSuccess ? e : hipGetLastError();
   }
   if constexpr (sizeof(T) == 4) {
-    if (a.ABT) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
+    if (MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE) {
+      if (a.ABT) hipLaunchKernelGGL((riccati_kernel_f32<true, true>), dim3(g64), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((riccati_kernel_f32<false, true>), dim3(g64), dim3(64), 0, st, a);
+    } else {
+      if (a.ABT) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
+    }
   } else {
     // one fp64 instantiation (export guarded at run time): measured leaner than the export-free
     // one, which LLVM schedules into 368 bytes of scratch spill
-    hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
+    if (MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE)
+      hipLaunchKernelGGL((riccati_kernel_f64<true, true>), dim3(g64), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
