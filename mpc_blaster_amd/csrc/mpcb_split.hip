@@ -465,11 +465,12 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   const T* xr = a.xref + b * a.xref_sb;
   const T* ur = a.uref + b * a.uref_sb;
   const T hv = (a.h / T(6)) * T(6);   // the RK4 tangent's position entry of a velocity column
-  // fp64: the model constants of the tangent (J, Jinv, arm lengths, 1/m) as opaque loop-invariant
-  // VGPR pairs instead of kernel-argument SGPR pairs (MPCB_P2_MVGPR, default on): 44 SGPRs the
-  // body otherwise spills to VGPR lanes and reads back at every stage
+  // fp64 and the fp32 export instantiation: the model constants of the tangent (J, Jinv, arm
+  // lengths, 1/m) as opaque loop-invariant VGPRs instead of kernel-argument SGPRs (MPCB_P2_MVGPR,
+  // default on): scalar registers the body otherwise spills to VGPR lanes and reads back at every
+  // stage (fp64 22 -> 0 spills, fp32 export 14 -> 0)
   Model<T> Mv = a.M;
-  if constexpr (sizeof(T) == 8 && MPCB_P2_MVGPR) {
+  if constexpr ((sizeof(T) == 8 || EXPORT) && MPCB_P2_MVGPR) {
     asm volatile("" : "+v"(Mv.minv), "+v"(Mv.lx), "+v"(Mv.ly), "+v"(Mv.c));
 #pragma unroll
     for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(Mv.J[i]), "+v"(Mv.Jinv[i]));
