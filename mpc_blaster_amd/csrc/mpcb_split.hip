@@ -59,6 +59,9 @@
 #ifndef MPCB_P2_WAVES_F32
 #define MPCB_P2_WAVES_F32 2
 #endif
+#ifndef MPCB_P2_WAVES_F32_NOEXP   // the export-free fp32 instantiation (c3, c5)
+#define MPCB_P2_WAVES_F32_NOEXP 2
+#endif
 
 namespace mpcb {
 
@@ -965,7 +968,7 @@ template <class T, bool USE_CC, bool ITER>
 __global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC, ITER>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
 template <bool EXPORT, bool ITER = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_P2_WAVES_F32, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EXPORT ? MPCB_P2_WAVES_F32 : MPCB_P2_WAVES_F32_NOEXP, 8)))
 riccati_kernel_f32(SplitArgs<float> a) {
   riccati_body<float, EXPORT, ITER>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
