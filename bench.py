@@ -85,10 +85,29 @@ def cpu_baseline(w, budget_s=12.0):
     done, t_used = timed(cores, 4096 if not w['box'] else 2048, 0.75 * budget_s)
     done1, t1 = timed(1, 256, 0.25 * budget_s)
     what = 'input-box active set' if w['box'] else ('wind' if w['wind'] else 'unconstrained')
-    return dict(value=done / t_used, unit='solves/s', cores=cores, kind='port',
-                value_1thread=done1 / t1,
-                sample=f'{done} instances of {w["name"]} (N={w["N"]}, fp64, plain-C oracle oracle/c, '
-                       f'{what}, OpenMP) in {t_used:.1f} s; 1 thread: {done1} in {t1:.1f} s')
+    out = dict(value=done / t_used, unit='solves/s', cores=cores, kind='port',
+               value_1thread=done1 / t1,
+               sample=f'{done} instances of {w["name"]} (N={w["N"]}, fp64, plain-C oracle oracle/c, '
+                      f'{what}, OpenMP) in {t_used:.1f} s; 1 thread: {done1} in {t1:.1f} s')
+    if w['name'] == 'c2':
+        out['c1_latency_ms'] = c1_latency()
+    return out
+
+
+def c1_latency(reps=2000):
+    """SURVEY §8d's CPU figure at the c1 shape (BASELINE configs[0]: 1 instance, N=10, fp64,
+    hover reference): per-instance latency of the plain-C port on ONE thread, each solve timed
+    inside C (oracle/c mpc_oracle_latency_b1), over 256 seeded x0 draws cycled ``reps`` times --
+    the per-control-step cost the reference's loop (simulation_blaster.py:56-107) pays, next to
+    the GPU's ``latency_b1``."""
+    from oracle import c_oracle
+    from oracle.inputs import make_inputs
+    from oracle.ocp import OcpSpec
+    inp = make_inputs('c1', ids=np.arange(256, dtype=np.uint64), N=10)
+    ms = c_oracle.latency_b1(inp['x0'], inp['xref'], inp['uref'], OcpSpec(N=10), reps=reps)
+    return dict(median=float(np.median(ms)), p99=float(np.percentile(ms, 99)), mean=float(ms.mean()),
+                threads=1, reps=int(reps), N=10,
+                sample='c1 shape: 1 instance per solve, N=10, fp64, hover ref, 256 seeded x0 (seed 1001)')
 
 
 class _DeviceClock:
@@ -386,6 +405,10 @@ def main():
     ap.add_argument('--no-latency', action='store_true', help='skip the B=1 per-step latency block')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     ap.add_argument('--max-as-iter', type=int, default=200, help='active-set cap (box workload)')
+    ap.add_argument('--secondary-batch', type=int, default=None,
+                    help='per-GPU batch of the secondary workload (default: its BASELINE size)')
+    ap.add_argument('--init-timeout', type=float, default=120.0,
+                    help='seconds a rank waits for the others to join the process group')
     # launcher test only (tests/test_bench_launch.py): gloo ranks on the CPU with a stand-in solver
     ap.add_argument('--backend', default='nccl', choices=('nccl', 'gloo'), help=argparse.SUPPRESS)
     ap.add_argument('--solver-stub', default=None, help=argparse.SUPPRESS)
@@ -420,23 +443,44 @@ def main():
         dev = torch.cuda.current_device()
     else:
         dev = 'cpu'
+    if args.solver_stub:   # imported before the rendezvous (the launcher test's stalled-rank case)
+        import importlib
+        importlib.import_module(args.solver_stub)
     if world > 1:
+        # a rank that never joins makes the others fail within init_timeout (non-zero exit, and
+        # torch.distributed.run then stops the remaining ranks) instead of hanging to the
+        # driver's limit with no JSON line
+        from datetime import timedelta
+        tmo = timedelta(seconds=args.init_timeout)
         if cuda and args.backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device(f'cuda:{gpu}'))
+            dist.init_process_group('nccl', device_id=torch.device(f'cuda:{gpu}'), timeout=tmo)
         else:
-            dist.init_process_group('gloo')
+            dist.init_process_group('gloo', timeout=tmo)
 
     r = run(w, world, rank, dev, args.steps, args.warmup, stub=args.solver_stub,
             dump_gather=args.dump_gather)
+    # the secondary line: the BASELINE config quoted at this GPU count, so that the driver's
+    # 1/4/8-GPU runs each time the config named for that count -- c3 (configs[2], 1 GPU), c4
+    # (configs[3]: 262144 instances sharded over 4 GPUs, input box) and c5 (configs[4]: 1048576
+    # over 8 GPUs, RCCL all_reduce of the u0* histogram)
     sec = None
-    if world == 1 and cuda and not args.no_secondary and args.workload == 'c2':
-        w3 = dict(WORKLOADS['c3'], name='c3')
-        r3 = run(w3, 1, 0, dev, args.steps, args.warmup)
-        v3, roof3 = summarize(w3, r3, 1, args.steps)
-        roof3.pop('note')
-        sec = {'workload': 'c3: batch 65536/GPU, N=20, fp32, sinusoidal refs (BASELINE configs[2])',
-               'value': v3, 'unit': 'solves/s', 'ms_per_step': r3['elapsed'] / args.steps * 1e3,
-               'dtype': 'f32', 'path': r3['path'], 'roofline': roof3, 'bad_status': r3['bad']}
+    sec_name = {1: 'c3', 4: 'c4', 8: 'c5'}.get(world)
+    if sec_name and args.workload == 'c2' and not args.no_secondary and (cuda or world > 1):
+        ws = dict(WORKLOADS[sec_name], name=sec_name, max_as_iter=args.max_as_iter)
+        if args.secondary_batch:
+            ws['batch'] = args.secondary_batch
+        rs = run(ws, world, rank, dev, args.steps, args.warmup, stub=args.solver_stub,
+                 dump_gather=(args.dump_gather + '.secondary.npy') if args.dump_gather else None)
+        if rank == 0:
+            vs, roofs = summarize(ws, rs, world, args.steps)
+            roofs.pop('note')
+            desc = {'c3': 'BASELINE configs[2]: N=20, fp32, sinusoidal refs',
+                    'c4': 'BASELINE configs[3]: N=30, fp32, input box [0,65] N, instance-sharded',
+                    'c5': 'BASELINE configs[4]: N=40, fp32, wind sweep, u0* histogram all_reduce'}[sec_name]
+            sec = {'workload': f'{sec_name}: batch {ws["batch"]}/GPU ({desc})',
+                   'global_batch': ws['batch'] * world, 'n_gpus': world,
+                   'value': vs, 'unit': 'solves/s', 'ms_per_step': rs['elapsed'] / args.steps * 1e3,
+                   'dtype': ws['dtype'], 'path': rs['path'], 'roofline': roofs, 'bad_status': rs['bad']}
 
     if rank == 0:
         coll = 'RCCL' if args.backend == 'nccl' else 'gloo'

@@ -18,7 +18,10 @@
  *    synchronises to keep acados' synchronous semantics.
  *  - A handle is bound to one device, owns its workspace, and is not re-entrant.
  *  - Per-instance ``status`` (acados codes: 0 success, 1 NaN detected, 2 max iterations,
- *    4 QP failure) is separate from the call-level return code.
+ *    3 MINSTEP, 4 QP failure) is separate from the call-level return code.
+ *  - Arrays handed to a setter (mpcb_set_params) are read by later solves, not copied: the
+ *    caller keeps them alive and unchanged until the next set call (the Python facade passes a
+ *    private copy, so it keeps acados' copy semantics of ``set``).
  */
 #ifndef MPCB_H
 #define MPCB_H
@@ -42,8 +45,10 @@ enum {
 };
 /* per-instance solver status, acados' codes (ACADOS_SUCCESS, _NAN_DETECTED, _MAXITER, _MINSTEP,
  * _QP_FAILURE).  MINSTEP: the fp64 17/6 interior point stopped at its conditioning limit (a
- * breakdown or collapsed step once mu <= 1e-5 on a feasible iterate) and the active-set polish did
- * not certify the point: the outputs are that reduced-accuracy iterate. */
+ * breakdown or collapsed step once mu <= 1e-5 on a feasible iterate) and no active-set polish
+ * certified the point: the outputs are that reduced-accuracy iterate.  With the state box the
+ * polish runs first (MINSTEP = it did not certify); the input box alone (Mehrotra) has no polish,
+ * so every such stop there reports MINSTEP (oracle: ocp._ipm_box_mehrotra, the same rule). */
 enum { MPCB_STATUS_OK = 0, MPCB_STATUS_NAN = 1, MPCB_STATUS_MAXITER = 2, MPCB_STATUS_MINSTEP = 3,
        MPCB_STATUS_QP_FAIL = 4 };
 

@@ -80,6 +80,8 @@ class BatchedMPC:
     def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):
         """Coerce to a contiguous device tensor of the handle dtype; return (tensor, stride)."""
         torch = _torch()
+        if isinstance(t, np.ndarray) and not t.flags.writeable:
+            t = t.copy()   # torch.as_tensor warns on read-only arrays
         t = torch.as_tensor(t, dtype=self.dtype, device=f'cuda:{self.device}')
         if t.dim() == len(shape_tail):
             t = t.unsqueeze(0)
@@ -175,6 +177,8 @@ class BatchedMPC:
             return
         torch = _torch()
         N = self.cfg.N
+        if isinstance(p, np.ndarray) and not p.flags.writeable:
+            p = p.copy()   # torch.as_tensor warns on read-only arrays
         t = torch.as_tensor(p, dtype=self.dtype, device=f'cuda:{self.device}')
         if t.dim() == 1:
             t = t.reshape(1, 1, -1)
@@ -182,7 +186,9 @@ class BatchedMPC:
             t = t.unsqueeze(1)
         if t.dim() != 3 or t.shape[-1] != 25 or t.shape[1] not in (1, N, N + 1):
             raise ValueError(f'p: expected [25], [B|1, 25] or [B|1, N|N+1, 25], got {tuple(p.shape)}')
-        t = t.contiguous()
+        # acados ``set`` copies: a private device copy, so later writes to the caller's tensor
+        # do not reach the solver (the library reads the pointer at every solve, mpcb.h)
+        t = t.contiguous().clone()
         self._params = t   # the library keeps the device pointer: hold the tensor
         rows, stages = t.shape[0], t.shape[1]
         sb = 0 if rows == 1 else stages * 25

@@ -110,10 +110,10 @@ class AcadosOcpSolver:
                     raise NotImplementedError('stage-0 state box must be an equality (lbx_0 == ubx_0)')
                 self.x0 = v.copy()
         elif field == 'x':
-            self.xbar[:, stage] = torch.as_tensor(_slice_x(value, self.B, 'x', self.nx),
+            self.xbar[:, stage] = torch.as_tensor(np.array(_slice_x(value, self.B, 'x', self.nx)),
                                                   dtype=self.xbar.dtype, device=self._dev)
         elif field == 'u':
-            self.ubar[:, stage] = torch.as_tensor(_slice_u(value, self.B, 'u', self.nu),
+            self.ubar[:, stage] = torch.as_tensor(np.array(_slice_u(value, self.B, 'u', self.nu)),
                                                   dtype=self.ubar.dtype, device=self._dev)
         elif field == 'p':
             if not 0 <= stage <= self.N:

@@ -14,8 +14,6 @@ change the reference's OCP).
 """
 from __future__ import annotations
 
-import warnings
-
 import numpy as np
 
 from ..config import NU, NU17, NX, NX17, MPCConfig
@@ -51,8 +49,11 @@ class blasterModel:  # noqa: N801  (reference class name)
         sb = self._statesBound
         if sb.shape == (2, NX17) and np.isfinite(sb).all() and self._controlBound.size > 0:
             if self._dtype != 'f64':
-                warnings.warn('statesBound needs dtype f64 on the device; not applied in fp32', stacklevel=3)
-                return {}
+                # one policy with the 12/4 slice: a silently unenforced constraint would change
+                # the reference's OCP (blastermodel.py:268-270)
+                raise NotImplementedError('statesBound (blastermodel.py:268-270): the state box needs '
+                                 "dtype='f64' on the device; pass a non-finite statesBound to "
+                                 'solve without it in fp32')
             return dict(lbx=sb[0].copy(), ubx=sb[1].copy())
         return {}
 

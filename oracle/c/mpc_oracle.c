@@ -12,7 +12,9 @@
  * and Murty's least-index backup of oracle/ocp.py pdas_solve, over the masked Riccati recursion.
  * Parallel over instances with OpenMP (one instance per thread at a time).
  */
+#define _POSIX_C_SOURCE 199309L
 #include <math.h>
+#include <time.h>
 #include <string.h>
 
 #define NX 12
@@ -426,5 +428,28 @@ int mpc_oracle_solve(int B, int N, const oracle_params* P, const double* x0, con
     }
     free(work);
   }
+  return bad;
+}
+
+/* Per-instance latency at the c1 shape (the reference's one-solve-per-control-step
+ * loop simulation_blaster.py:56-107): R single-instance solves on the calling thread, each timed
+ * with CLOCK_MONOTONIC into ns[r] (instance r % B of x0, so the draws vary).  No Python in the
+ * timed region.  Returns the number of failed solves. */
+int mpc_oracle_latency_b1(int B, int N, const oracle_params* P, const double* x0, const double* xref,
+                          const double* uref, int R, double* ns) {
+  const size_t wsz = (size_t)(N + 1) * NX + (size_t)N * NX * NZ + (size_t)N * NU * NX + (size_t)N * NU;
+  double* work = (double*)malloc(sizeof(double) * wsz);
+  double* X = (double*)malloc(sizeof(double) * (size_t)(N + 1) * NX);
+  double* U = (double*)malloc(sizeof(double) * (size_t)N * NU);
+  double u0[NU];
+  int bad = 0;
+  for (int r = 0; r < R; ++r) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    bad += solve_one(N, P, x0 + (size_t)(r % B) * NX, xref, uref, NULL, u0, X, U, work) != 0;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    ns[r] = (double)(t1.tv_sec - t0.tv_sec) * 1e9 + (double)(t1.tv_nsec - t0.tv_nsec);
+  }
+  free(work); free(X); free(U);
   return bad;
 }

@@ -10,7 +10,7 @@ import numpy as np
 from .ocp import OcpSpec
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, 'c', 'libmpc_oracle.so')
+LIB = os.environ.get('MPCB_ORACLE_LIB') or os.path.join(_HERE, 'c', 'libmpc_oracle.so')
 
 
 class _Params(ctypes.Structure):
@@ -88,3 +88,23 @@ def solve(x0, xref, uref, spec: OcpSpec, nthreads: int = 1, want_traj: bool = Tr
                          ptr(u0), ptr(X), ptr(U),
                          st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.c_int(nthreads))
     return dict(u0=u0, X=X, U=U, status=st)
+
+
+def latency_b1(x0, xref, uref, spec: OcpSpec, reps: int = 2000):
+    """Per-instance solve latency of the plain-C port on the calling thread (c1 shape: one
+    instance per call, as the reference's control loop simulation_blaster.py:56-107 solves it):
+    ``reps`` single-instance solves cycling over the rows of ``x0`` (broadcast xref/uref), each
+    timed inside C.  Returns the per-solve times in ms."""
+    lib = load()
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    xr = np.ascontiguousarray(np.asarray(xref, dtype=np.float64)[:1])
+    ur = np.ascontiguousarray(np.asarray(uref, dtype=np.float64)[:1])
+    ns = np.empty(int(reps))
+    P = _params(spec)
+    dp = ctypes.POINTER(ctypes.c_double)
+    bad = lib.mpc_oracle_latency_b1(ctypes.c_int(x0.shape[0]), ctypes.c_int(spec.N), ctypes.byref(P),
+                                    x0.ctypes.data_as(dp), xr.ctypes.data_as(dp), ur.ctypes.data_as(dp),
+                                    ctypes.c_int(int(reps)), ns.ctypes.data_as(dp))
+    if bad:
+        raise RuntimeError(f'{bad} failed solves in the latency sample')
+    return ns * 1e-6

@@ -7,11 +7,21 @@ rank's global ids, so the gathered u0 can be compared with an unsharded oracle s
 """
 from __future__ import annotations
 
+import os
+import time
+
 import numpy as np
 import torch
 
 from oracle.inputs import make_inputs
 from oracle.ocp import OcpSpec, mpc_solve
+
+
+# the stalled-rank case of the launcher test: this rank never reaches the rendezvous (bench.py
+# imports the stub before init_process_group), so the others must fail within --init-timeout
+if os.environ.get('BENCH_STUB_STALL_RANK') not in (None, '') and \
+        os.environ.get('RANK') == os.environ['BENCH_STUB_STALL_RANK']:
+    time.sleep(3600)
 
 
 class _StubSolver:

@@ -13,17 +13,22 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run_bench(tmp_path, workload, gpus, batch, steps=2):
-    dump = str(tmp_path / f'gather_{workload}.npy')
+def _bench_cmd(workload, gpus, batch, steps, extra=()):
     env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get('PYTHONPATH', ''),
                OMP_NUM_THREADS='1')
-    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT', 'BENCH_STUB_STALL_RANK'):
         env.pop(k, None)
-    p = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', str(gpus),
-                        '--steps', str(steps), '--warmup', '1', '--workload', workload,
-                        '--batch', str(batch), '--no-cpu-baseline', '--backend', 'gloo',
-                        '--solver-stub', 'tests.bench_stub', '--dump-gather', dump],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    cmd = [sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', str(gpus),
+           '--steps', str(steps), '--warmup', '1', '--workload', workload,
+           '--batch', str(batch), '--no-cpu-baseline', '--backend', 'gloo',
+           '--solver-stub', 'tests.bench_stub'] + list(extra)
+    return cmd, env
+
+
+def _run_bench(tmp_path, workload, gpus, batch, steps=2, extra=()):
+    dump = str(tmp_path / f'gather_{workload}.npy')
+    cmd, env = _bench_cmd(workload, gpus, batch, steps, list(extra) + ['--dump-gather', dump])
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
     assert len(lines) == 1, p.stdout
@@ -54,3 +59,36 @@ def test_bench_gpus_1_runs_in_process(tmp_path):
     line, got = _run_bench(tmp_path, 'c2', 1, 8, steps=1)
     assert line['n_gpus'] == 1 and line['config']['global_batch'] == 8
     assert got.shape == (8, 4)
+
+
+def test_bench_gpus_4_adds_the_c4_secondary(tmp_path):
+    """At 4 ranks the line also times BASELINE configs[3] (c4: input box, instance-sharded over 4
+    GPUs); the gathered c4 u0 equals the unsharded oracle's active-set solution."""
+    from oracle.inputs import make_inputs
+    from oracle.ocp import OcpSpec, mpc_solve
+    sb = 3
+    line, _ = _run_bench(tmp_path, 'c2', 4, 4, steps=1, extra=['--secondary-batch', str(sb)])
+    assert line['n_gpus'] == 4 and line['config']['global_batch'] == 16
+    sec = line['secondary']
+    assert sec['workload'].startswith('c4') and sec['global_batch'] == 4 * sb and sec['n_gpus'] == 4
+    assert sec['value'] > 0 and sec['bad_status'] == 0
+    assert 'active_set' in sec['roofline']
+    got = np.load(str(tmp_path / 'gather_c2.npy') + '.secondary.npy')
+    inp = make_inputs('c4', ids=np.arange(4 * sb, dtype=np.uint64), N=30)
+    ref = mpc_solve(inp['x0'], inp['xref'], inp['uref'],
+                    OcpSpec(N=30, lbu=np.zeros(4), ubu=np.full(4, 65.0)))['u0']
+    assert got.shape == (4 * sb, 4)
+    assert np.array_equal(got, ref)
+
+
+def test_bench_stalled_rank_fails_fast():
+    """A rank that never joins the rendezvous: the others give up after --init-timeout and the
+    parent exits non-zero well before the driver's limit (no hang, no JSON line)."""
+    import time
+    cmd, env = _bench_cmd('c2', 2, 4, 1, ['--init-timeout', '8'])
+    env['BENCH_STUB_STALL_RANK'] = '1'
+    t0 = time.time()
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert time.time() - t0 < 200

@@ -32,3 +32,14 @@ def test_c_oracle_box_matches_numpy_pdas():
     for k in ('u0', 'X', 'U'):
         err = np.abs(a[k] - b[k]).max() / max(np.abs(a[k]).max(), 1.0)
         assert err < 1e-11, (k, err)
+
+
+def test_c_oracle_latency_b1_runs_single_instances():
+    """The c1-shape latency sampler (bench.py cpu_baseline.c1_latency_ms): one instance per C call,
+    every solve OK, positive per-solve times."""
+    from oracle import c_oracle
+    from oracle.inputs import make_inputs
+    from oracle.ocp import OcpSpec
+    inp = make_inputs('c1', ids=np.arange(4, dtype=np.uint64), N=10)
+    ms = c_oracle.latency_b1(inp['x0'], inp['xref'], inp['uref'], OcpSpec(N=10), reps=16)
+    assert ms.shape == (16,) and (ms > 0).all() and (ms < 1000).all()

@@ -125,3 +125,18 @@ def test_slice_refuses_a_finite_state_box():
     b2 = blasterModel(*_reference_args())
     b2.generateModel()
     assert b2._cfg.nx == 17 and b2._cfg.lbx is not None
+
+
+def test_fp32_refuses_a_finite_state_box():
+    """One constraint policy: the 17/6 state box is fp64-only on the device, so
+    an fp32 model with the reference's finite statesBound raises like the 12/4 slice does instead
+    of warning and solving without it; a non-finite statesBound is accepted in fp32."""
+    b = blasterModel(*_reference_args(), dtype='f32')
+    with pytest.raises(NotImplementedError, match='statesBound'):
+        b.generateModel()
+        b.generateController()
+    args = list(_reference_args())
+    args[11] = np.full_like(np.asarray(args[11], dtype=np.float64), np.inf)
+    b2 = blasterModel(*args, dtype='f32')
+    b2.generateModel()
+    assert b2._cfg.lbx is None
