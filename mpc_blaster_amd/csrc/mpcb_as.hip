@@ -188,7 +188,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   T* const PX = lds_px[q];
   const int64_t nb = a.nb;
   const int N = a.N;
-  const T h = a.h;
+  // the RK4 tangent's position entry of a velocity column, h/6 * (1 + 2 + 2 + 1) as the tangent
+  // computes it: the same [A|B] column as P2's (mpcb_split.hip riccati_body hv), whose snapshots
+  // the first masked pass restarts from
+  const T h = (a.h / T(6)) * T(6);
   const Weights<T>& W = *a.W;
   const bool iterate = MPCB_AS_ITER_T ? ITER : a.mode == MPCB_MODE_ITERATE;   // (see riccati_body)
   const T lbm = W.lbu[ju], ubm = W.ubu[ju];
@@ -233,6 +236,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     wave_lds_sync();
   }
   // row i of [A|B] at the constant columns (state lanes): position e_p, velocity e_v + h e_p
+  // (h: the tangent's h/6 * 6, above)
   T crow[6];
 #pragma unroll
   for (int p = 0; p < 3; ++p) {

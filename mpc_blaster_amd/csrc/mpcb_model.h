@@ -120,8 +120,11 @@ __device__ __forceinline__ void sc(float a, float* s, float* c) {
 }
 
 // 1/x by the hardware reciprocal and two Newton steps (fp64: v_rcp_f64 + 4 FMAs, ~1 ulp; the
-// IEEE division sequence is ~11 instructions with its scale / fixup steps).  |x| is cos(theta) of a
-// flying attitude here, far from 0, denormals and infinity.  MPCB_IEEE_DIV=1 restores the division.
+// IEEE division sequence is ~11 instructions with its scale / fixup steps).  Domain: normal, finite,
+// non-zero x -- cos(theta) of a flying attitude, and the 17/6 interior point's strictly positive
+// slacks and multipliers (mpcb_r17.hip, which keeps them >= a positive floor before taking
+// reciprocals).  recip(0) is NaN, not inf (fma(-0, inf, 1) = NaN): callers whose argument can
+// reach 0 or a denormal must use safe_recip.  MPCB_IEEE_DIV=1 restores the division.
 #ifndef MPCB_IEEE_DIV
 #define MPCB_IEEE_DIV 0
 #endif
@@ -134,6 +137,9 @@ __device__ __forceinline__ double recip(double x) {
   return fma(fma(-x, r, 1.0), r, r);
 #endif
 }
+// 1/x that keeps IEEE semantics at 0 / denormals / inf (the division) for arguments outside
+// recip()'s domain
+template <class T> __device__ __forceinline__ T safe_recip(T x) { return T(1) / x; }
 __device__ __forceinline__ float recip(float x) {
 #if MPCB_IEEE_DIV
   return 1.0f / x;

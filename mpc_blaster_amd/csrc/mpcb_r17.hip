@@ -1228,7 +1228,7 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
       // step length: fraction tau to the boundary, primal and dual, common to the instance
       // (the ratio tests as in the predictor: the largest -dv / v, from tau; amax = 1 / that)
       T ram = T(IPM17_TAU);
-      bool dfin = true;   // a finite direction from strictly positive slacks
+      bool dfin = true;   // a finite direction from strictly positive slacks and multipliers
       if (in && !parked) {
 #pragma unroll 4
         for (int k = 0; k < N; ++k) {
@@ -1244,7 +1244,9 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
             targets(smu, sl, su, ll, lu, da, -da, tl, tu, isl, isu);
           }
           const T dll = (tl - ll * sl - ll * d) * isl, dlu = (tu - lu * su + lu * d) * isu;
-          dfin = dfin && sl > T(0) && su > T(0) && isfin(d) && isfin(dll) && isfin(dlu);
+          // (recip() is NaN at 0, which fmax would drop from the ratio test: a multiplier that
+          // reached 0 is a breakdown, not an unlimited step -- ADVICE r3)
+          dfin = dfin && sl > T(0) && su > T(0) && ll > T(0) && lu > T(0) && isfin(d) && isfin(dll) && isfin(dlu);
           ram = fmax(ram, fmax(fmax(-d * isl, d * isu), fmax(-dll * recip(ll), -dlu * recip(lu))));
         }
       }
@@ -1256,7 +1258,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
           const T isl = recip(sr.sl), isu = recip(sr.su);
           const T dll = (smu - sr.ll * sr.sl - sr.ll * dsl) * isl;
           const T dlu = (smu - sr.lu * sr.su - sr.lu * dsu) * isu;
-          dfin = dfin && isfin(dsl) && isfin(dsu) && isfin(dll) && isfin(dlu);
+          dfin = dfin && sr.sl > T(0) && sr.su > T(0) && sr.ll > T(0) && sr.lu > T(0) && isfin(dsl) &&
+                 isfin(dsu) && isfin(dll) && isfin(dlu);
           ram = fmax(ram, fmax(fmax(-dsl * isl, -dsu * isu), fmax(-dll * recip(sr.ll), -dlu * recip(sr.lu))));
         };
 #pragma unroll 4

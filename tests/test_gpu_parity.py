@@ -494,3 +494,47 @@ def test_acados_facade_runs_reference_loop(t_blast):
         xs = rk4_step(xs[None], o['u0'], 1.0 / 30.0, P)[0]
         assert np.abs(x[:12] - xs).max() < 1e-9
     assert ocp_solver.mpc._h.value == handle     # T_blast changed in place, not by re-creation
+
+
+@pytest.mark.parametrize('dtype', ['f32', 'f64'])
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_box_long_horizon_w64_matches_oracle(dtype, mode):
+    """The 64-bit stage-mask active-set kernels (as_kernel_*<false, *>, 32 < N <= 64):
+    the reference horizon N=60 with the input box, ragged B, both modes, against the oracle; and
+    the work-counter grid bit-identical to one wave per quad (MPCB_AS_PERSIST=0) on the same
+    instantiation."""
+    N, B = 60, 157
+    inp = make_inputs('c4', ids=np.arange(B, dtype=np.uint64), N=N)
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    m = _mpc(N, dtype, box=True, max_batch=B, path='split')
+    kw = {}
+    if mode == 'iterate':
+        rng = np.random.default_rng(60)
+        kw = dict(xbar=cast(inp['xref'] + rng.normal(scale=0.05, size=(B, N + 1, 12))),
+                  ubar=cast(inp['uref'] + rng.normal(scale=2.0, size=(B, N, 4))))
+    res = []
+    for persist in ('1', '0'):
+        os.environ['MPCB_AS_PERSIST'] = persist
+        try:
+            if mode == 'iterate':
+                m.solve_iterate(inp['x0'], kw['xbar'], kw['ubar'], inp['xref'], inp['uref'])
+            else:
+                m.solve(inp['x0'], inp['xref'], inp['uref'])
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop('MPCB_AS_PERSIST')
+        res.append((m.get_control().clone(), m.get_input_trajectory().clone(),
+                    m.get_state_trajectory().clone(), m.get_status().clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    u0, U, X, st = (t.double().cpu().numpy() if t.is_floating_point() else t.cpu().numpy() for t in res[0])
+    o = mpc_solve(cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), _spec(N, box=True),
+                  mode=mode, **kw)
+    tol = 5e-5 if dtype == 'f32' else 1e-9
+    assert (st == o['status']).all()
+    ok = o['status'] == 0
+    assert ok.sum() >= B - 2
+    e_u, e_U, e_x = relerr(u0, o['u0'])[ok], relerr(U, o['U'])[ok], relerr(X, o['X'])[ok]
+    print(f'box N={N} {dtype} {mode}: max rel err u0 {e_u.max():.2e} U {e_U.max():.2e} X {e_x.max():.2e}')
+    assert e_u.max() < tol and e_U.max() < tol and e_x.max() < tol
+    assert (U >= -1e-5).all() and (U <= 65 + 1e-4).all()
