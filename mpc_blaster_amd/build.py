@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-SOURCES = ['mpcb_solve.hip', 'mpcb_split.hip', 'mpcb_box.hip', 'mpcb_as.hip', 'mpcb_aux.hip', 'mpcb_full.hip', 'mpcb_r17.hip',
+SOURCES = ['mpcb_solve.hip', 'mpcb_split.hip', 'mpcb_rollout.hip', 'mpcb_box.hip', 'mpcb_as.hip', 'mpcb_aux.hip', 'mpcb_full.hip', 'mpcb_r17.hip',
            'mpcb_poc.hip', 'mpcb_capi.hip']
 OUT = os.path.join(HERE, 'libmpcblaster.so')
 ARCH = os.environ.get('MPCB_OFFLOAD_ARCH', 'gfx950')

@@ -243,7 +243,10 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     h->fwd16 = (!cfg->box_u && !h->small && chunk <= fwd16_max) ? 1 : 0;
     int64_t quad_max = 16384;   // the rollout with a lane quad per instance (latency-bound sizes)
     if (const char* e = getenv("MPCB_QUAD_P1_MAX")) quad_max = atoll(e);
-    h->quad_p1 = (chunk <= quad_max) ? 1 : 0;
+    // the 16-lane row rollout (f split over the lanes, mpcb_rollout.hip) below MPCB_ROW_P1_MAX
+    int64_t row_max = 16384;
+    if (const char* e = getenv("MPCB_ROW_P1_MAX")) row_max = atoll(e);
+    h->quad_p1 = (chunk <= row_max) ? 2 : (chunk <= quad_max) ? 1 : 0;
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);

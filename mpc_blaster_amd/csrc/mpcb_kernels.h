@@ -31,7 +31,9 @@ struct SolveArgs {
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
-  int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
+  int quad_p1;       // P1 variant: 2 = a 16-lane row per instance (f split over the lanes,
+                     // mpcb_rollout.hip), 1 = a lane quad per instance (sin/cos split), 0 = a
+                     // thread per instance
   T h;               // RK4 step
   T s;               // stage cost scaling
   Model<T> M;
@@ -119,7 +121,9 @@ struct SplitArgs {
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
-  int quad_p1;       // 1: the rollout runs a lane quad per instance (sin/cos split over lanes)
+  int quad_p1;       // P1 variant: 2 = a 16-lane row per instance (f split over the lanes,
+                     // mpcb_rollout.hip), 1 = a lane quad per instance (sin/cos split), 0 = a
+                     // thread per instance
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
   int rm;            // 1: P2 writes the row-major exports (AB2, ABT2, GH2, KR2 in a.AB/a.ABT/a.GH/a.KR)
   int imajor;        // row-major exports instance-major (an instance's N records contiguous: the
@@ -134,6 +138,7 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st);
+template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStream_t st);   // mpcb_rollout.hip
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance
 template <class T> int64_t solve_slot_elems(int N, int box);
 

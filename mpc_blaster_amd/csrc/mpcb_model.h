@@ -76,9 +76,16 @@ struct ScRegs {
   __device__ __forceinline__ double s(int i) const { return vs[i]; }
   __device__ __forceinline__ double c(int i) const { return vc[i]; }
 };
+// MPCB_SC_FALLBACK=0: no large-argument fallback (instruction counting of the fast path only:
+// tools/isa_loop.py; never a shipped build)
+#ifndef MPCB_SC_FALLBACK
+#define MPCB_SC_FALLBACK 1
+#endif
 template <class K>
 __device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
+#if MPCB_SC_FALLBACK
   if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
+#endif
   const double n = rint(a * 6.36619772367581382433e-01);           // 2/pi
   double r = fma(-n, 1.57079632673412561417e+00, a);              // pio2_1 (33 bits)
   r = fma(-n, 6.07710050650619224932e-11, r);                     // pio2_1t
@@ -105,7 +112,9 @@ __device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
 }
 __device__ __forceinline__ void sc(double a, double* s, double* c) { sc(a, s, c, ScConst{}); }
 __device__ __forceinline__ void sc(float a, float* s, float* c) {
+#if MPCB_SC_FALLBACK
   if (!(fabsf(a) < 8192.0f)) { sincosf(a, s, c); return; }
+#endif
   const float n = rintf(a * 0.636619772367581343f);
   float r = fmaf(-n, 1.57079637050628662109375f, a);              // pio2 hi
   r = fmaf(-n, -4.37113900018624283e-08f, r);                     // pio2 lo

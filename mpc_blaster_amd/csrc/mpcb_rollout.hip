@@ -1,0 +1,235 @@
+// mpcb_rollout.hip — P1 of the split path with a 16-lane row per instance (small chunks: c2).
+//
+// The nominal RK4 rollout of the linearisation point (acados sim_erk on the OCP of
+// blastermodel.py:214-292; dynamics f_expl_expr, blastermodel.py:95-201) is a serial chain of
+// 4·N evaluations of f per instance.  At c2 (4096 instances) the lane-quad rollout
+// (nominal_quad_kernel, mpcb_split.hip) fills 256 wavefronts — one SIMD in four — and each of
+// them issues the whole of f for 16 instances, because the quad's lanes only split the sin/cos.
+// Here the 16 lanes of a row SPLIT f itself, so a wavefront carries 4 instances (one workspace
+// quad) and c2 runs 1024 wavefronts, one per SIMD, each with a chain about half as long:
+//
+//   lane t < 12 holds state x_t and computes f_t; lanes 12..15 hold u_{t-12} (f = 0 there);
+//   every lane takes sin/cos of its own state (lanes 3, 4, 5: phi, theta, psi) and lane 4 the
+//   reciprocal 1/cos(theta); row broadcasts (v_mov_b64_dpp row_newbcast) give every lane the
+//   eleven scalars the row shares (sin/cos of the three angles, 1/cos(theta), tan(theta), the
+//   body rates); the few products of f that several rows share (a, b, the rotation column
+//   R e3) are formed once per lane; then lane t's row of f is assembled from them by FMAs with
+//   loop-invariant per-lane 0/1 coefficients (and, for the body rates, the per-lane quadratic
+//   form of -J^-1 (w x J w) plus the per-interval J^-1 M(u));
+//   the RK4 stage update of x_t is lane-local.
+//
+// The captured linearisation scalars (mpcb_model.h f_nom_lin: 20 per RK stage) are stored from
+// the lanes that hold them into the same quad-blocked CC record the other P1 variants write, so
+// P2 is unchanged; likewise XU (x_k, u_k) and, in iterate mode, the gaps GP.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcb.h"
+#include "mpcb_common.h"
+#include "mpcb_kernels.h"
+#include "mpcb_split.h"
+
+namespace mpcb {
+
+namespace {
+
+// lane L's value in every lane of its 16-lane row (fp64: one v_mov_b64_dpp)
+template <int L, class T> __device__ __forceinline__ T rbc(T v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);   // (no old value to zero)
+}
+// lane t + 6's value in lane t of the row (row_shl:6; lanes 10..15 read 0)
+template <class T> __device__ __forceinline__ T shl6(T v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true);
+}
+
+template <class T> struct ScOf { using type = ScConst; };
+template <> struct ScOf<double> { using type = ScRegs; };
+
+}  // namespace
+
+// DJ: diagonal inertia (the reference's J, simulation_blaster.py:13-15): the gyroscopic term of
+// body rate t is one product (w_{t+1} w_{t+2}); otherwise the general six-product quadratic form.
+template <class T, bool ITER, bool DJ>
+__global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
+  const int lane = threadIdx.x;
+  const int t = lane & 15;                 // row lane
+  const int q = lane >> 4;                 // instance within the wavefront's quad
+  const int64_t nb = a.nb;
+  const int64_t nq = (nb + SS - 1) / SS;
+  const int64_t qd = blockIdx.x;           // the wavefront's workspace quad
+  const int64_t c_raw = qd * SS + q;
+  const int64_t c = c_raw < nb ? c_raw : nb - 1;   // ragged quad: recompute the last instance
+  const int64_t b = a.b0 + c;
+  const int N = a.N;
+  const Model<T>& M = a.M;
+  const T h = a.h, h2 = T(0.5) * a.h, h6 = a.h / T(6);
+
+  // ---- loop-invariant per-lane coefficients (0/1 row selectors, J-dependent forms) ----------
+  const T kv = T(t < 3);                   // f_t = v_t (t < 3), from lane t + 6
+  const T k1 = T(t == 3);                  // f_3 = wx + tt a
+  const T k2 = T(t == 3), k3 = T(t == 5);  // f_5 = ict a
+  const T k4 = T(t == 4);                  // f_4 = b
+  const T kr0 = T(t == 6), kr1 = T(t == 7), kr2 = T(t == 8);   // f_{6+i} = s r_i + const
+  // body rates t = 9..11: f = J^-1 M(u) - J^-1 (w x J w).  (w x Jw)_i = sum_jl B_i[j][l] w_j w_l
+  // with B_i[j][l] = sum_m eps_ijm J_ml; the per-lane form over the products
+  // p = (w0 w0, w1 w1, w2 w2, w0 w1, w0 w2, w1 w2) is G_t,p = -sum_i Jinv[t-9][i] coef_i,p
+  T G[6];
+  T Lm[4];   // J^-1 mixer: f_t's constant part is sum_m Lm[m] u_m
+  {
+    const int r = (t >= 9 && t < 12) ? t - 9 : -1;
+    T coef[3][6];
+    auto Jm = [&](int m, int l) { return M.J[m * 3 + l]; };
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;   // eps_{i,i1,i2} = +1, eps_{i,i2,i1} = -1
+      auto B = [&](int j, int l) {
+        return (j == i1 ? Jm(i2, l) : T(0)) - (j == i2 ? Jm(i1, l) : T(0));
+      };
+      coef[i][0] = B(0, 0); coef[i][1] = B(1, 1); coef[i][2] = B(2, 2);
+      coef[i][3] = B(0, 1) + B(1, 0); coef[i][4] = B(0, 2) + B(2, 0); coef[i][5] = B(1, 2) + B(2, 1);
+    }
+    // mixer (blastermodel.py:95-101): M = [ly(u1+u3-u0-u2), lx(u1+u2-u0-u3), c(u2+u3-u0-u1)]
+    const T mix[3][4] = {{-M.ly, M.ly, -M.ly, M.ly}, {-M.lx, M.lx, M.lx, -M.lx}, {-M.c, -M.c, M.c, M.c}};
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      T g = T(0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) g += (r >= 0 ? M.Jinv[r * 3 + i] : T(0)) * coef[i][p];
+      G[p] = -g;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T l = T(0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) l += (r >= 0 ? M.Jinv[r * 3 + i] : T(0)) * mix[i][m];
+      Lm[m] = l;
+    }
+  }
+  // the lane's row of J (captured J w, mpcb_model.h f_nom_lin c[14..16]) on lanes 9..11
+  const int jr = (t >= 9 && t < 12) ? t - 9 : 0;
+  const T J0 = M.J[jr * 3], J1 = M.J[jr * 3 + 1], J2 = M.J[jr * 3 + 2];
+  // constant part of f_t: the wind force / m and gravity (t = 6..8)
+  T K0 = T(0);
+  if (a.wind && t >= 6 && t < 9) K0 = a.wind[b * a.wind_sb + (t - 6)] * M.minv;
+  if (t == 8) K0 -= M.g;
+  const typename ScOf<T>::type kc;
+
+  // ---- workspace addressing: the quad-blocked records of mpcb_split.h soa(), quad qd --------
+  T* const xu0 = a.XU + qd * XU_REC * SS + q;
+  T* const cc0 = a.CC + qd * CCS_REC * SS + q;
+  T* const gp0 = ITER ? a.GP + qd * GP_REC * SS + q : nullptr;
+  const int64_t xu_k = nq * XU_REC * SS, cc_k = nq * CCS_REC * SS, gp_k = nq * GP_REC * SS;
+
+  const T* xbp = a.xbar + b * (int64_t)(N + 1) * NX;
+  const T* ubp = a.ubar + b * (int64_t)N * NU;
+  const T* ur = a.uref + b * a.uref_sb;
+  // X: x_t (t < 12) / u_{t-12} (t >= 12) of the interval's start
+  T X = T(0);
+  if (t < NX) X = ITER ? xbp[t] : a.x0[b * a.x0_sb + t];
+
+  for (int k = 0; k < N; ++k) {
+    if (ITER && t < NX && k) X = xbp[(int64_t)k * NX + t];
+    if (t >= NX) X = ITER ? ubp[(int64_t)k * NU + (t - NX)] : ur[(int64_t)k * NU + (t - NX)];
+    xu0[k * xu_k + t * SS] = X;
+    // per-interval constants: the inputs, the thrust scale and J^-1 M(u) + the constant forces
+    const T u0 = rbc<12>(X), u1 = rbc<13>(X), u2 = rbc<14>(X), u3 = rbc<15>(X);
+    const T s = ((u0 + u1) + (u2 + u3) + M.t_blast) * M.minv;
+    const T Kt = fma(Lm[0], u0, fma(Lm[1], u1, fma(Lm[2], u2, fma(Lm[3], u3, K0))));
+    T* const cck = cc0 + k * cc_k;
+    T Y = X, XN = T(0), Xn = T(0);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      // sin/cos of the lane's own state (lanes 3..5: the Euler angles), 1/cos and tan on lane 4
+      T S, C;
+      if constexpr (sizeof(T) == 8) sc(Y, &S, &C, kc);
+      else sc(Y, &S, &C);
+      const T R = recip(C);
+      const T Tn = S * R;
+      const T sf = rbc<3>(S), cf = rbc<3>(C), sth = rbc<4>(S), cth = rbc<4>(C);
+      const T sp = rbc<5>(S), cp = rbc<5>(C), ict = rbc<4>(R), tt = rbc<4>(Tn);
+      const T wx = rbc<9>(Y), wy = rbc<10>(Y), wz = rbc<11>(Y);
+      const T av = sf * wy + cf * wz;
+      const T bv = cf * wy - sf * wz;
+      const T cfst = cf * sth;
+      const T r0 = cp * cfst + sp * sf;
+      const T r1 = sp * cfst - cp * sf;
+      const T r2 = cf * cth;
+      // lane t's row of f
+      T F = fma(kv, shl6(Y), Kt);
+      F = fma(k4, bv, F);
+      F = fma(av, fma(k2, tt, k3 * ict), F);
+      F = fma(k1, wx, F);
+      F = fma(s, fma(kr0, r0, fma(kr1, r1, kr2 * r2)), F);
+      if constexpr (DJ) {
+        F = fma(G[5], wy * wz, F);
+        F = fma(G[4], wx * wz, F);
+        F = fma(G[3], wx * wy, F);
+      } else {
+        F = fma(G[0], wx * wx, F);
+        F = fma(G[1], wy * wy, F);
+        F = fma(G[2], wz * wz, F);
+        F = fma(G[3], wx * wy, F);
+        F = fma(G[4], wx * wz, F);
+        F = fma(G[5], wy * wz, F);
+      }
+      const T JW = fma(J0, wx, fma(J1, wy, J2 * wz));
+      // captured scalars of this RK stage (f_nom_lin order), each from a lane that holds it
+      T* const cs = cck + st * LIN_N * SS;
+      if (t >= 3 && t < 6) {
+        cs[(2 * (t - 3)) * SS] = S;          // sf, st, sp
+        cs[(2 * (t - 3) + 1) * SS] = C;      // cf, ct, cp
+      }
+      if (t == 4) {
+        cs[6 * SS] = R;                      // ict
+        cs[7 * SS] = Tn;                     // tt
+      }
+      if (t >= 9 && t < 12) {
+        cs[(t + 5) * SS] = JW;               // jw0..2
+        cs[(t + 8) * SS] = Y;                // wx, wy, wz
+      }
+      if (t == 0) {
+        cs[8 * SS] = av;
+        cs[9 * SS] = cfst;
+        cs[10 * SS] = s;
+        cs[11 * SS] = r0;
+        cs[12 * SS] = r1;
+        cs[13 * SS] = r2;
+      }
+      // RK4 stage update (lane-local; f = 0 on the input lanes)
+      if (st == 0) { XN = F; Y = fma(h2, F, X); }
+      else if (st == 1) { XN = fma(T(2), F, XN); Y = fma(h2, F, X); }
+      else if (st == 2) { XN = fma(T(2), F, XN); Y = fma(h, F, X); }
+      else Xn = fma(h6, XN + F, X);
+    }
+    if (ITER) {
+      if (t < NX) gp0[k * gp_k + t * SS] = Xn - xbp[(int64_t)(k + 1) * NX + t];
+    } else if (t < NX) {
+      X = Xn;
+    }
+  }
+  if (t < NX) {
+    if (ITER) X = xbp[(int64_t)N * NX + t];
+  } else {
+    X = T(0);
+  }
+  xu0[N * xu_k + t * SS] = X;
+}
+
+template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
+  const bool dj = a.M.J[1] == T(0) && a.M.J[2] == T(0) && a.M.J[3] == T(0) && a.M.J[5] == T(0) &&
+                  a.M.J[6] == T(0) && a.M.J[7] == T(0);
+  const bool it = a.mode == MPCB_MODE_ITERATE;
+  if (dj) {
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true>), grid, dim3(64), 0, st, a);
+  } else {
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false>), grid, dim3(64), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+template hipError_t launch_nominal_row<double>(const SplitArgs<double>&, hipStream_t);
+template hipError_t launch_nominal_row<float>(const SplitArgs<float>&, hipStream_t);
+
+}  // namespace mpcb

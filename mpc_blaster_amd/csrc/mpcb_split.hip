@@ -998,7 +998,10 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (a.quad_p1) {
+  if (a.quad_p1 == 2) {
+    const hipError_t e = launch_nominal_row<T>(a, st);
+    if (e != hipSuccess) return e;
+  } else if (a.quad_p1) {
     const dim3 gq((unsigned)((a.nb + QI - 1) / QI));
     if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((nominal_quad_kernel<T, true>), gq, dim3(WAVE), 0, st, a);
     else hipLaunchKernelGGL((nominal_quad_kernel<T, false>), gq, dim3(WAVE), 0, st, a);

@@ -9,7 +9,7 @@ import re,collections,sys
 s=open(sys.argv[1]).read(); name=sys.argv[2]
 i=s.index(name+':'); j=s.index('.Lfunc_end',i)
 L=[l.strip() for l in s[i:j].split('\n')]
-hdrs=[l for l in L if 'This Loop Header: Depth=1' in l and 'Inner' not in l]
+hdrs=[l for l in L if 'Loop Header: Depth=1' in l]
 bb=hdrs[0].split(':')[0][2:]
 blocks=[];cur=None
 for k,l in enumerate(L):
