@@ -64,6 +64,7 @@ struct mpcb_handle {
   int split;              // 1: three-kernel split path; 0: single-kernel solver (boxes)
   int small;              // split path, small unconstrained chunks: cached-[A|B] passes
   int fwd16;              // split path, small chunks: P2 exports [A|B]^T for a 16-lane forward
+  int tin;                // split path: the row rollout exports [A|B] (SplitArgs::tin)
   int quad_p1;            // split path, small chunks: rollout with a lane quad per instance
   int64_t chunk;          // split path: instances per chunk
   int64_t chunk_elems;    // elements of the chunk workspace (XU | CC | GP | KR)
@@ -247,7 +248,13 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     int64_t row_max = 16384;
     if (const char* e = getenv("MPCB_ROW_P1_MAX")) row_max = atoll(e);
     h->quad_p1 = (chunk <= row_max) ? 2 : (chunk <= quad_max) ? 1 : 0;
-    const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16) ? 1 : 0);
+    // the row rollout also integrates the tangents and exports [A|B] (MPCB_P1_TAN: default on in
+    // fp64; in fp32 its regrouped tangent algebra doubled the worst U error of the N=60 box test,
+    // 3.7e-5 -> 7.3e-5 against the 5e-5 bound, so fp32 keeps the captured scalars); P2 then reads
+    // [A|B] instead of integrating it
+    h->tin = (h->quad_p1 == 2 && !h->small && f64) ? 1 : 0;
+    if (const char* e = getenv("MPCB_P1_TAN")) if (atoi(e) == 0) h->tin = 0;
+    const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
     // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
@@ -403,6 +410,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.small = h->small;
       a.fwd16 = h->fwd16;
       a.quad_p1 = h->quad_p1;
+      a.tin = h->tin;
       T* ab = a.GP + (int64_t)N * nbp * GP_REC;
       // row-major exports for the active-set kernel and the 16-lane forward pass; the optional
       // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
@@ -410,7 +418,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.imajor = h->cfg.box_u ? 0 : 1;
       if (const char* e = getenv("MPCB_RM_IMAJOR")) a.imajor = atoi(e) != 0;
       a.AB = ((h->cfg.box_u && MPCB_AS_AB2) || h->small) ? ab : nullptr;
-      a.ABT = (h->cfg.box_u || h->small || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
+      a.ABT = (h->cfg.box_u || h->small || h->tin || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH2_REC : nullptr;
       a.qp_stats = h->qp_stats;

@@ -46,9 +46,66 @@ template <> struct ScOf<double> { using type = ScRegs; };
 
 }  // namespace
 
+// Tangent of one RK stage along the lane's direction (TAN): dk = J_f(x_s, u)·(dS, e_u) from the
+// stage's scalars, which every lane of the row already holds after the broadcasts (the algebra of
+// mpcb_model.h f_tan_lin, regrouped around the products the nominal f shares: with the lane's input
+// direction a constant, dT·minv and J^-1 M(du) are loop-invariant per lane).  DJ: diagonal J, so
+// (w x Jw)' is (J_a - J_b)(w_b dw_c + dw_b w_c) per component.
+template <class T> struct StageSc {
+  T sf, cf, st, ct, sp, cp, ict, tt, a, b, cfst, s, r0, r1, r2, wx, wy, wz, jw0, jw1, jw2;
+};
+template <class T> struct TanConst {
+  T dsl;             // dT · minv of the lane's input direction (0 on state lanes)
+  T Ju[3];           // J^-1 M(e_u) of the lane's input direction
+  T kd[3];           // DJ: -Jinv_ii (J_a - J_b)
+  T J[9], Ji[9];     // general J
+};
+template <class T, bool DJ>
+__device__ __forceinline__ void tan_stage(const StageSc<T>& c, const T* __restrict__ dS,
+                                          const TanConst<T>& K, T* __restrict__ dk) {
+  const T dphi = dS[3], dth = dS[4], dpsi = dS[5];
+  const T dwx = dS[9], dwy = dS[10], dwz = dS[11];
+  const T ict2st = c.ict * c.ict * c.st;                 // d(1/ct)/dth
+  const T dict = ict2st * dth;
+  const T dtt = fma(c.ct * c.ict, dth, c.st * dict);     // dst ict + st dict
+  const T da = fma(dphi, c.b, fma(c.sf, dwy, c.cf * dwz));
+  const T db = fma(-dphi, c.a, fma(c.cf, dwy, -c.sf * dwz));
+  dk[0] = dS[6]; dk[1] = dS[7]; dk[2] = dS[8];
+  dk[3] = fma(dtt, c.a, fma(c.tt, da, dwx));
+  dk[4] = db;
+  dk[5] = fma(da, c.ict, c.a * dict);
+  const T dcfst = fma(c.r2, dth, -(c.sf * c.st) * dphi);   // dcf st + cf dst
+  const T dr0 = fma(-dpsi, c.r1, fma(c.cp, dcfst, (c.sp * c.cf) * dphi));
+  const T dr1 = fma(dpsi, c.r0, fma(c.sp, dcfst, -(c.cp * c.cf) * dphi));
+  const T dr2 = -fma(c.sf * c.ct, dphi, c.cfst * dth);
+  dk[6] = fma(dr0, c.s, c.r0 * K.dsl);
+  dk[7] = fma(dr1, c.s, c.r1 * K.dsl);
+  dk[8] = fma(dr2, c.s, c.r2 * K.dsl);
+  if constexpr (DJ) {
+    dk[9] = fma(K.kd[0], fma(dwy, c.wz, c.wy * dwz), K.Ju[0]);
+    dk[10] = fma(K.kd[1], fma(dwz, c.wx, c.wz * dwx), K.Ju[1]);
+    dk[11] = fma(K.kd[2], fma(dwx, c.wy, c.wx * dwy), K.Ju[2]);
+  } else {
+    const T djw0 = fma(K.J[0], dwx, fma(K.J[1], dwy, K.J[2] * dwz));
+    const T djw1 = fma(K.J[3], dwx, fma(K.J[4], dwy, K.J[5] * dwz));
+    const T djw2 = fma(K.J[6], dwx, fma(K.J[7], dwy, K.J[8] * dwz));
+    const T dc0 = fma(dwy, c.jw2, c.wy * djw2) - fma(dwz, c.jw1, c.wz * djw1);
+    const T dc1 = fma(dwz, c.jw0, c.wz * djw0) - fma(dwx, c.jw2, c.wx * djw2);
+    const T dc2 = fma(dwx, c.jw1, c.wx * djw1) - fma(dwy, c.jw0, c.wy * djw0);
+    dk[9] = K.Ju[0] - fma(K.Ji[0], dc0, fma(K.Ji[1], dc1, K.Ji[2] * dc2));
+    dk[10] = K.Ju[1] - fma(K.Ji[3], dc0, fma(K.Ji[4], dc1, K.Ji[5] * dc2));
+    dk[11] = K.Ju[2] - fma(K.Ji[6], dc0, fma(K.Ji[7], dc1, K.Ji[8] * dc2));
+  }
+}
+
 // DJ: diagonal inertia (the reference's J, simulation_blaster.py:13-15): the gyroscopic term of
 // body rate t is one product (w_{t+1} w_{t+2}); otherwise the general six-product quadratic form.
-template <class T, bool ITER, bool DJ>
+// TAN: the row also integrates the RK4 tangent of direction e_t (lane t; state lanes e_x, input
+// lanes e_u) through the same four stages and exports the variable columns of [A_k | B_k] as the
+// ABT2 rows (mpcb_kernels.h) that P2 then reads instead of integrating them (SplitArgs::tin).  The
+// tangent of stage s is independent of the nominal stage s + 1, so the two chains interleave in
+// one basic block; no captured-scalar record (CC) is written.
+template <class T, bool ITER, bool DJ, bool TAN>
 __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   const int lane = threadIdx.x;
   const int t = lane & 15;                 // row lane
@@ -112,10 +169,32 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   if (a.wind && t >= 6 && t < 9) K0 = a.wind[b * a.wind_sb + (t - 6)] * M.minv;
   if (t == 8) K0 -= M.g;
   const typename ScOf<T>::type kc;
+  // the tangent's lane constants (TAN): direction e_t; its input part e_{t-12} on lanes 12..15
+  TanConst<T> K{};
+  T ev[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) ev[i] = T(t == i);
+  if constexpr (TAN) {
+    const int m = t >= NX ? t - NX : -1;
+    K.dsl = m >= 0 ? M.minv : T(0);
+    const T mixm[3] = {m < 0 ? T(0) : ((m == 1 || m == 3) ? M.ly : -M.ly),
+                       m < 0 ? T(0) : ((m == 1 || m == 2) ? M.lx : -M.lx),
+                       m < 0 ? T(0) : ((m == 2 || m == 3) ? M.c : -M.c)};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      K.Ju[r] = fma(M.Jinv[r * 3], mixm[0], fma(M.Jinv[r * 3 + 1], mixm[1], M.Jinv[r * 3 + 2] * mixm[2]));
+    K.kd[0] = -M.Jinv[0] * (M.J[8] - M.J[4]);
+    K.kd[1] = -M.Jinv[4] * (M.J[0] - M.J[8]);
+    K.kd[2] = -M.Jinv[8] * (M.J[4] - M.J[0]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { K.J[i] = M.J[i]; K.Ji[i] = M.Jinv[i]; }
+  }
+  const int tv = var_index(t);             // the lane's variable column of [A|B] (-1: constant)
+  const bool exp_lane = TAN && tv >= 0 && c_raw < nb;
 
   // ---- workspace addressing: the quad-blocked records of mpcb_split.h soa(), quad qd --------
   T* const xu0 = a.XU + qd * XU_REC * SS + q;
-  T* const cc0 = a.CC + qd * CCS_REC * SS + q;
+  T* const cc0 = TAN ? nullptr : a.CC + qd * CCS_REC * SS + q;
   T* const gp0 = ITER ? a.GP + qd * GP_REC * SS + q : nullptr;
   const int64_t xu_k = nq * XU_REC * SS, cc_k = nq * CCS_REC * SS, gp_k = nq * GP_REC * SS;
 
@@ -134,8 +213,10 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
     const T u0 = rbc<12>(X), u1 = rbc<13>(X), u2 = rbc<14>(X), u3 = rbc<15>(X);
     const T s = ((u0 + u1) + (u2 + u3) + M.t_blast) * M.minv;
     const T Kt = fma(Lm[0], u0, fma(Lm[1], u1, fma(Lm[2], u2, fma(Lm[3], u3, K0))));
-    T* const cck = cc0 + k * cc_k;
     T Y = X, XN = T(0), Xn = T(0);
+    T dS[NX], dN[NX];   // TAN: the stage's tangent input and the RK4 accumulator
+#pragma unroll
+    for (int i = 0; i < NX; ++i) dS[i] = ev[i];
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       // sin/cos of the lane's own state (lanes 3..5: the Euler angles), 1/cos and tan on lane 4
@@ -144,61 +225,85 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
       else sc(Y, &S, &C);
       const T R = recip(C);
       const T Tn = S * R;
-      const T sf = rbc<3>(S), cf = rbc<3>(C), sth = rbc<4>(S), cth = rbc<4>(C);
-      const T sp = rbc<5>(S), cp = rbc<5>(C), ict = rbc<4>(R), tt = rbc<4>(Tn);
-      const T wx = rbc<9>(Y), wy = rbc<10>(Y), wz = rbc<11>(Y);
-      const T av = sf * wy + cf * wz;
-      const T bv = cf * wy - sf * wz;
-      const T cfst = cf * sth;
-      const T r0 = cp * cfst + sp * sf;
-      const T r1 = sp * cfst - cp * sf;
-      const T r2 = cf * cth;
-      // lane t's row of f
-      T F = fma(kv, shl6(Y), Kt);
-      F = fma(k4, bv, F);
-      F = fma(av, fma(k2, tt, k3 * ict), F);
-      F = fma(k1, wx, F);
-      F = fma(s, fma(kr0, r0, fma(kr1, r1, kr2 * r2)), F);
+      StageSc<T> c;
+      c.sf = rbc<3>(S); c.cf = rbc<3>(C); c.st = rbc<4>(S); c.ct = rbc<4>(C);
+      c.sp = rbc<5>(S); c.cp = rbc<5>(C); c.ict = rbc<4>(R); c.tt = rbc<4>(Tn);
+      c.wx = rbc<9>(Y); c.wy = rbc<10>(Y); c.wz = rbc<11>(Y);
+      c.a = c.sf * c.wy + c.cf * c.wz;
+      c.b = c.cf * c.wy - c.sf * c.wz;
+      c.cfst = c.cf * c.st;
+      c.r0 = c.cp * c.cfst + c.sp * c.sf;
+      c.r1 = c.sp * c.cfst - c.cp * c.sf;
+      c.r2 = c.cf * c.ct;
+      c.s = s;
+      // lane t's row of f, as three independent partial sums
+      T F0 = fma(kv, shl6(Y), Kt);
+      T F1 = fma(k4, c.b, k1 * c.wx);
+      T F2 = c.s * fma(kr0, c.r0, fma(kr1, c.r1, kr2 * c.r2));
+      F0 = fma(c.a, fma(k2, c.tt, k3 * c.ict), F0);
       if constexpr (DJ) {
-        F = fma(G[5], wy * wz, F);
-        F = fma(G[4], wx * wz, F);
-        F = fma(G[3], wx * wy, F);
+        F1 = fma(G[5], c.wy * c.wz, F1);
+        F2 = fma(G[4], c.wx * c.wz, F2);
+        F0 = fma(G[3], c.wx * c.wy, F0);
       } else {
-        F = fma(G[0], wx * wx, F);
-        F = fma(G[1], wy * wy, F);
-        F = fma(G[2], wz * wz, F);
-        F = fma(G[3], wx * wy, F);
-        F = fma(G[4], wx * wz, F);
-        F = fma(G[5], wy * wz, F);
+        F1 = fma(G[0], c.wx * c.wx, F1);
+        F2 = fma(G[1], c.wy * c.wy, F2);
+        F0 = fma(G[2], c.wz * c.wz, F0);
+        F1 = fma(G[3], c.wx * c.wy, F1);
+        F2 = fma(G[4], c.wx * c.wz, F2);
+        F0 = fma(G[5], c.wy * c.wz, F0);
       }
-      const T JW = fma(J0, wx, fma(J1, wy, J2 * wz));
-      // captured scalars of this RK stage (f_nom_lin order), each from a lane that holds it
-      T* const cs = cck + st * LIN_N * SS;
-      if (t >= 3 && t < 6) {
-        cs[(2 * (t - 3)) * SS] = S;          // sf, st, sp
-        cs[(2 * (t - 3) + 1) * SS] = C;      // cf, ct, cp
-      }
-      if (t == 4) {
-        cs[6 * SS] = R;                      // ict
-        cs[7 * SS] = Tn;                     // tt
-      }
-      if (t >= 9 && t < 12) {
-        cs[(t + 5) * SS] = JW;               // jw0..2
-        cs[(t + 8) * SS] = Y;                // wx, wy, wz
-      }
-      if (t == 0) {
-        cs[8 * SS] = av;
-        cs[9 * SS] = cfst;
-        cs[10 * SS] = s;
-        cs[11 * SS] = r0;
-        cs[12 * SS] = r1;
-        cs[13 * SS] = r2;
+      const T F = F0 + (F1 + F2);
+      const T JW = fma(J0, c.wx, fma(J1, c.wy, J2 * c.wz));
+      if constexpr (TAN) {
+        if constexpr (!DJ) { c.jw0 = rbc<9>(JW); c.jw1 = rbc<10>(JW); c.jw2 = rbc<11>(JW); }
+        T dk[NX];
+        tan_stage<T, DJ>(c, dS, K, dk);
+        // RK4 tangent update (mpcb_model.h rk4_tan: same operations)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          if (st == 0) { dN[i] = dk[i]; dS[i] = fma(h2, dk[i], ev[i]); }
+          else if (st == 1) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h2, dk[i], ev[i]); }
+          else if (st == 2) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h, dk[i], ev[i]); }
+          else dN[i] = fma(h6, dN[i] + dk[i], ev[i]);
+        }
+      } else {
+        // captured scalars of this RK stage (f_nom_lin order), each from a lane that holds it
+        T* const cs = cc0 + k * cc_k + st * LIN_N * SS;
+        if (t >= 3 && t < 6) {
+          cs[(2 * (t - 3)) * SS] = S;          // sf, st, sp
+          cs[(2 * (t - 3) + 1) * SS] = C;      // cf, ct, cp
+        }
+        if (t == 4) {
+          cs[6 * SS] = R;                      // ict
+          cs[7 * SS] = Tn;                     // tt
+        }
+        if (t >= 9 && t < 12) {
+          cs[(t + 5) * SS] = JW;               // jw0..2
+          cs[(t + 8) * SS] = Y;                // wx, wy, wz
+        }
+        if (t == 0) {
+          cs[8 * SS] = c.a;
+          cs[9 * SS] = c.cfst;
+          cs[10 * SS] = s;
+          cs[11 * SS] = c.r0;
+          cs[12 * SS] = c.r1;
+          cs[13 * SS] = c.r2;
+        }
       }
       // RK4 stage update (lane-local; f = 0 on the input lanes)
       if (st == 0) { XN = F; Y = fma(h2, F, X); }
       else if (st == 1) { XN = fma(T(2), F, XN); Y = fma(h2, F, X); }
       else if (st == 2) { XN = fma(T(2), F, XN); Y = fma(h, F, X); }
       else Xn = fma(h6, XN + F, X);
+    }
+    if constexpr (TAN) {
+      // column var_col(tv) of [A_k | B_k] into the ABT2 rows: entry (i, tv) at i * ABT2_W + tv
+      if (exp_lane) {
+        T* const abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor) + tv;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) abt[i * ABT2_W] = dN[i];
+      }
     }
     if (ITER) {
       if (t < NX) gp0[k * gp_k + t * SS] = Xn - xbp[(int64_t)(k + 1) * NX + t];
@@ -214,18 +319,27 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   xu0[N * xu_k + t * SS] = X;
 }
 
-template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStream_t st) {
+template <class T, bool TAN>
+static void launch_row_m(const SplitArgs<T>& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
-  const bool dj = a.M.J[1] == T(0) && a.M.J[2] == T(0) && a.M.J[3] == T(0) && a.M.J[5] == T(0) &&
-                  a.M.J[6] == T(0) && a.M.J[7] == T(0);
+  // diagonal J (and J^-1): the gyroscopic products and their tangent shrink to one term per rate
+  bool dj = true;
+  for (int i = 0; i < 9; ++i)
+    if (i % 4 != 0) dj = dj && a.M.J[i] == T(0) && a.M.Jinv[i] == T(0);
   const bool it = a.mode == MPCB_MODE_ITERATE;
   if (dj) {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true>), grid, dim3(64), 0, st, a);
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true, TAN>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true, TAN>), grid, dim3(64), 0, st, a);
   } else {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false>), grid, dim3(64), 0, st, a);
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false, TAN>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false, TAN>), grid, dim3(64), 0, st, a);
   }
+}
+
+template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStream_t st) {
+  // (the tangent export is built for fp64 only: mpcb_create sets tin there)
+  if (sizeof(T) == 8 && a.tin) launch_row_m<T, sizeof(T) == 8>(a, st);
+  else launch_row_m<T, false>(a, st);
   return hipGetLastError();
 }
 

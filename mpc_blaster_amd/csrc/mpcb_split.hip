@@ -20,6 +20,7 @@
 #include "../../include/mpcb.h"
 #include "mpcb_common.h"
 #include "mpcb_split.h"
+#include "mpcb_dpp_gen.h"
 
 // fp64 Riccati products through DPP row broadcasts (1) or LDS operands (0, the earlier path)
 #ifndef MPCB_P2_DPP
@@ -448,8 +449,21 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
 #ifndef MPCB_P2_MVGPR
 #define MPCB_P2_MVGPR 1
 #endif
-template <class T, bool EXPORT, bool ITER = false>
+// TIN: the row rollout already integrated the tangents (SplitArgs::tin): column j of [A|B] comes
+// from its ABT2 rows (variable directions) or is the constant e_j / e_j + hv e_{j-6} (the others),
+// prefetched one stage ahead like the captured scalars it replaces
+// lane L's value in every lane of its 16-lane row (one v_mov_b64_dpp row_newbcast)
+template <int L> __device__ __forceinline__ double rbc64(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
+}
+
+template <class T, bool EXPORT, bool ITER = false, bool TIN = false>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
+  // fp64 DPP path: every exchange of the stage by row broadcasts -- Y reads P straight out of
+  // the lanes' unsymmetrised columns (lane max(i, l) owns entry (i, l): mpcb_dpp_gen.h ypn_bc),
+  // the stage-cost term S v, H_uu and h_u by broadcasts -- so P needs no LDS transpose and the
+  // stage no LDS round trip (the box path's snapshots still publish P through LDS)
+  constexpr bool D64 = sizeof(T) == 8 && MPCB_P2_DPP;
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
   const int q = lane >> 4;
@@ -515,18 +529,32 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   // group stride padded so that two groups' broadcast reads of the same scalar fall on different
   // banks (96 elements put them on one bank: a 2-way conflict on every tangent read)
   __shared__ T Cst[2][GROUPS][CCS_REC + NZ + MPCB_P2_CPAD];
-  T pc[5], pyb, pyr, pgp = T(0);
-  auto prefetch = [&](int k) {
-    const T* cc = soa(a.CC, k, CCS_REC, nb, c);
+  T pc[TIN ? NX : 5], pyb, pyr, pgp = T(0);
+  const int tvj = var_index(j);
+  const T kvar = T(tvj >= 0);   // TIN: 1 on the variable directions, 0 on the constant ones
+  T ce[NX];                     // TIN: the constant column (0 on the variable directions)
 #pragma unroll
-    for (int r = 0; r < 5; ++r) pc[r] = cc[(j + 16 * r) * SS];
+  for (int i = 0; i < NX; ++i)
+    ce[i] = (tvj >= 0) ? T(0) : ((i == j) ? T(1) : (j >= 6 && j < 9 && i == j - 6) ? hv : T(0));
+  auto prefetch = [&](int k) {
+    if constexpr (TIN) {
+      const T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor) + (tvj >= 0 ? tvj : 0);
+#pragma unroll
+      for (int i = 0; i < NX; ++i) pc[i] = abt[i * ABT2_W];
+    } else {
+      const T* cc = soa(a.CC, k, CCS_REC, nb, c);
+#pragma unroll
+      for (int r = 0; r < 5; ++r) pc[r] = cc[(j + 16 * r) * SS];
+    }
     pyb = soa(a.XU, k, XU_REC, nb, c)[j * SS];
     pyr = *((j < NX) ? xr + (int64_t)k * NX + jx : ur + (int64_t)k * NU + ju);
     if (iterate) pgp = soa(a.GP, k, GP_REC, nb, c)[jx * SS];   // input lanes: unused copy
   };
   auto commit = [&](int bufi) {
+    if constexpr (!TIN) {
 #pragma unroll
-    for (int r = 0; r < 5; ++r) Cst[bufi][q][j + 16 * r] = pc[r];
+      for (int r = 0; r < 5; ++r) Cst[bufi][q][j + 16 * r] = pc[r];
+    }
     Cst[bufi][q][CCS_REC + j] = pgp;
   };
   prefetch(N - 1);
@@ -536,23 +564,29 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   wave_lds_sync();
   STAMP_INIT();
   for (int k = N - 1; k >= 0; --k) {
+    T col[NX];
+    if constexpr (TIN) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) col[i] = fma(kvar, pc[i], ce[i]);
+    }
     if (k > 0) prefetch(k - 1);
     STAMP(0);
-    T col[NX];
     {
       const T* cc = &Cst[buf][q][0];
-      L.v[j] = cyb - cyr;
-      T dx[NX], du[NU];
+      if constexpr (!D64) L.v[j] = cyb - cyr;
+      if constexpr (!TIN) {
+        T dx[NX], du[NU];
 #pragma unroll
-      for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
+        for (int i = 0; i < NX; ++i) dx[i] = (j == i) ? T(1) : T(0);
 #pragma unroll
-      for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
-      rk4_tan<T>(cc, dx, du, a.h, Mv, col);
+        for (int m = 0; m < NU; ++m) du[m] = (j == NX + m) ? T(1) : T(0);
+        rk4_tan<T>(cc, dx, du, a.h, Mv, col);
+      }
       STAMP(1);
-      const int tv = var_index(j);   // exported: the state-dependent columns only
+      const int tv = tvj;   // exported: the state-dependent columns only
       if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
         if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c, N, a.imajor) + tv * NX, col);
-        if (a.ABT && valid && tv >= 0) {
+        if (!TIN && a.ABT && valid && tv >= 0) {
           T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor);
 #pragma unroll
           for (int i = 0; i < NX; ++i) abt[i * ABT2_W + tv] = col[i];
@@ -563,18 +597,20 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
           for (int i = 0; i < NX; ++i) ab[(i * NVAR + tv) * SS] = col[i];
         }
-        if (EXPORT && a.ABT && valid && tv >= 0) {
+        if (!TIN && EXPORT && a.ABT && valid && tv >= 0) {
           T* abt = soa(a.ABT, k, AB_REC, nb, c);
 #pragma unroll
           for (int i = 0; i < NX; ++i) abt[(tv * NX + i) * SS] = col[i];
         }
       }
-      T pt = pj;
-      if (iterate) {
+      if constexpr (!D64) {
+        T pt = pj;
+        if (iterate) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pt += Pc[i] * cc[CCS_REC + i];
+          for (int i = 0; i < NX; ++i) pt += Pc[i] * cc[CCS_REC + i];
+        }
+        L.hv[j] = pt;
       }
-      L.hv[j] = pt;
     }
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // LDS-operand fp64 products
 #pragma unroll
@@ -592,8 +628,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       for (int i = 0; i < NX; ++i) y[i] = 0.0;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) g[i] = 0.0;
-      const double ptl = L.hv[j];
-      static_for<NX>([&](auto l) { fmac13_bc<decltype(l)::value>(y, hj, Pc, ptl, col[l]); });
+      // h = [A|B]^T (p + P gap) = col_j . p + Y_j . gap  (P symmetric)
+      static_for<NX>([&](auto l) { ypn_bc<decltype(l)::value>(y, hj, Pc, pj, col[l]); });
+      if (iterate) {
+        const T* cc = &Cst[buf][q][0];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) hj = fma(y[i], cc[CCS_REC + i], hj);
+      }
 #if MPCB_P2_GVAR
       // rows of G at the 10 variable directions by broadcasts; the 6 constant ones from Y alone:
       // column e_p of [A|B] gives G[p][j] = Y[p][j], column e_v + hv e_p (hv = the tangent's
@@ -643,28 +684,48 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       }
     }
     STAMP(3);
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      // SW is symmetric: lane j reads column j so the 16 lanes hit 16 consecutive entries (row j
-      // put every second lane on the same bank: an 8-way conflict on each of these reads)
-      const T w = MPCB_P2_SWT ? SW[i * NZ + j] : SW[j * NZ + i];
-      G[i] += w;
-      hj += w * L.v[i];
-    }
-    // (box path: no Hessian rows here -- the active set is empty in this pass, and the first
-    // masked backward recomputes every stage and writes the rows its fixed components need)
-#pragma unroll
-    for (int m = 0; m < NU; ++m) L.Hu[j * HS + m] = G[NX + m];
-    wave_lds_sync();
-    L.hv[j] = hj;
-    wave_lds_sync();
-    STAMP(4);
     T Huu[NU * NU], hu[NU];
+    if constexpr (D64) {
+      // stage cost: G += s blkdiag(Q, R) (lane j: column j), h += (s blkdiag(Q, R) v)_j with v_i
+      // broadcast from lane i; then H_uu and h_u from the input lanes by broadcasts
+      double sw[NZ];
 #pragma unroll
-    for (int m = 0; m < NU; ++m) {
+      for (int i = 0; i < NZ; ++i) sw[i] = SW[i * NZ + j];
 #pragma unroll
-      for (int n = 0; n < NU; ++n) Huu[m * NU + n] = L.Hu[(NX + n) * HS + m];
-      hu[m] = -L.hv[NX + m];
+      for (int i = 0; i < NZ; ++i) G[i] += sw[i];
+      double acc4[4] = {hj, 0.0, 0.0, 0.0};
+      dot16_bc(acc4, cyb - cyr, sw);
+      hj = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+      STAMP(4);
+      static_for<NU>([&](auto n) {
+        constexpr int nn = decltype(n)::value;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) Huu[m * NU + nn] = rbc64<NX + nn>(G[NX + m]);
+        hu[nn] = -rbc64<NX + nn>(hj);
+      });
+    } else {
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) {
+        // SW is symmetric: lane j reads column j so the 16 lanes hit 16 consecutive entries (row j
+        // put every second lane on the same bank: an 8-way conflict on each of these reads)
+        const T w = MPCB_P2_SWT ? SW[i * NZ + j] : SW[j * NZ + i];
+        G[i] += w;
+        hj += w * L.v[i];
+      }
+      // (box path: no Hessian rows here -- the active set is empty in this pass, and the first
+      // masked backward recomputes every stage and writes the rows its fixed components need)
+#pragma unroll
+      for (int m = 0; m < NU; ++m) L.Hu[j * HS + m] = G[NX + m];
+      wave_lds_sync();
+      L.hv[j] = hj;
+      wave_lds_sync();
+      STAMP(4);
+#pragma unroll
+      for (int m = 0; m < NU; ++m) {
+#pragma unroll
+        for (int n = 0; n < NU; ++n) Huu[m * NU + n] = L.Hu[(NX + n) * HS + m];
+        hu[m] = -L.hv[NX + m];
+      }
     }
     T Lc[10];
     chol4(Huu, Lc);
@@ -699,7 +760,17 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     STAMP(6);
     kff0 = sel<NU>(kff, ju);
-    if (valid && a.rm) {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
+    if (D64 && (TIN || a.rm)) {
+      // KR2 (TIN: always this layout), four stores from every lane and no lane branch, so the
+      // next stage's wait for its prefetched loads counts exactly these stores (a path without
+      // them made the compiler wait for every store to complete, vmcnt(0)): state lane j writes
+      // K[m][j]; input lane ju k_ju to slot 12 of row ju and its other three stores to the
+      // rows' pad slot 13.  Padding groups write the same values as the instance they repeat.
+      T* kr = rec2(a.KR, k, KR2_REC, nb, c, N, a.imajor);
+#pragma unroll
+      for (int m = 0; m < NU; ++m)
+        kr[m * KR2_W + (j < NX ? j : (m == ju ? 12 : 13))] = (j < NX) ? Kj[m] : kff0;
+    } else if (valid && a.rm) {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
       T* kr = rec2(a.KR, k, KR2_REC, nb, c, N, a.imajor);
       if (j < NX) {
 #pragma unroll
@@ -723,8 +794,11 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     // lane publishes its column and takes the entries below its diagonal from the lanes that
     // own them: uniform code instead of per-entry predicated stores.  (L.X is free: this
     // stage's products are done.)
+    const bool publish = !D64 || (EXPORT && a.PS);   // D64: only the box path's snapshots
+    if (publish) {
 #pragma unroll
-    for (int i = 0; i < NX; ++i) L.X[j * XS + i] = Pn[i];
+      for (int i = 0; i < NX; ++i) L.X[j * XS + i] = Pn[i];
+    }
     pj = pn;
     if (k > 0) commit(buf ^ 1);
     wave_lds_sync();
@@ -743,6 +817,10 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       stv<T, PS2_W>(rec2(a.PS, k, PS2_REC, nb, c, N, a.imajor) + j * PS2_W, ps);
     }
     STAMP(8);
+    if constexpr (D64) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) Pc[i] = Pn[i];   // unsymmetrised: ypn_bc reads the owners
+    } else {
 #if MPCB_P2_PCSEL
     {   // unconditional LDS reads + lane-mask selects (no exec-masked branch per entry)
       const uint64_t st_lane = lane_mask(j < NX);
@@ -756,6 +834,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
     for (int i = 0; i < NX; ++i) Pc[i] = (j < NX) ? ((i <= j) ? Pn[i] : L.X[i * XS + j]) : T(0);
 #endif
+    }
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // the LDS fp64 products read P from LDS
       if (j < NX) {
 #pragma unroll
@@ -967,14 +1046,14 @@ __global__ void __launch_bounds__(64) nominal_quad_kernel(SplitArgs<T> a) { nomi
 template <class T, bool USE_CC, bool ITER>
 __global__ void __launch_bounds__(64) forward_kernel(SplitArgs<T> a) { forward_wave<T, USE_CC, ITER>(a); }
 // register budget: fp32 at 2 waves/SIMD (measured faster than 3 with its small spill); fp64 uncapped
-template <bool EXPORT, bool ITER = false>
+template <bool EXPORT, bool ITER = false, bool TIN = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EXPORT ? MPCB_P2_WAVES_F32 : MPCB_P2_WAVES_F32_NOEXP, 8)))
 riccati_kernel_f32(SplitArgs<float> a) {
-  riccati_body<float, EXPORT, ITER>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  riccati_body<float, EXPORT, ITER, TIN>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
-template <bool EXPORT, bool ITER = false>
+template <bool EXPORT, bool ITER = false, bool TIN = false>
 __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs<double> a) {
-  riccati_body<double, EXPORT, ITER>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  riccati_body<double, EXPORT, ITER, TIN>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
 template <class T, bool USE_CC, bool ITER>
@@ -1017,8 +1096,9 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     if (ev) (void)hipEventRecord(ev[3], st);
     return e != hipSuccess ? e : hipGetLastError();
   }
+  const bool it = MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE;
   if constexpr (sizeof(T) == 4) {
-    if (MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE) {
+    if (it) {
       if (a.ABT) hipLaunchKernelGGL((riccati_kernel_f32<true, true>), dim3(g64), dim3(64), 0, st, a);
       else hipLaunchKernelGGL((riccati_kernel_f32<false, true>), dim3(g64), dim3(64), 0, st, a);
     } else {
@@ -1026,12 +1106,16 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
       else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
     }
   } else {
-    // one fp64 instantiation (export guarded at run time): measured leaner than the export-free
-    // one, which LLVM schedules into 368 bytes of scratch spill
-    if (MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE)
+    // one fp64 instantiation per mode (export guarded at run time): measured leaner than the
+    // export-free one, which LLVM schedules into 368 bytes of scratch spill
+    if (a.tin) {
+      if (it) hipLaunchKernelGGL((riccati_kernel_f64<true, true, true>), dim3(g64), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((riccati_kernel_f64<true, false, true>), dim3(g64), dim3(64), 0, st, a);
+    } else if (it) {
       hipLaunchKernelGGL((riccati_kernel_f64<true, true>), dim3(g64), dim3(64), 0, st, a);
-    else
+    } else {
       hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
+    }
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
