@@ -31,6 +31,11 @@ FLOP_PER_INTERVAL = 34785          # dense algorithmic flops p
 # the Riccati kernel (dominant): RK4 sensitivities (21,996) minus the 4 f evaluations the nominal
 # pass already did (4 x 300), plus the Riccati backward recursion (12,309)
 FLOP_PER_INTERVAL_RICCATI = 21996 - 4 * 300 + 12309
+# fp64 chunks <= 16384 (c2): the row rollout integrates the sensitivities itself and exports [A|B]
+# (mpcb_rollout.hip, SplitArgs::tin), so it carries the whole RK4 + sensitivity count and P2 the
+# Riccati backward alone
+FLOP_PER_INTERVAL_ROLLOUT_TAN = 21996
+FLOP_PER_INTERVAL_RICCATI_TIN = 12309
 PEAK_TFLOPS = {'f64': 78.6, 'f32': 157.3}   # MI355X dense vector (= matrix) peaks, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 
@@ -243,9 +248,11 @@ def phase_kernels(w):
     """rocprof names and algorithmic flop counts of the split path's three launches for this
     workload (the library picks the variants by chunk size: mpcb_capi.hip mpcb_create).
     Dense algorithmic counts per shooting interval:
-      nominal  4 f evaluations (4 x 300) of the RK4 rollout;
+      nominal  4 f evaluations (4 x 300) of the RK4 rollout; with the tangent export (fp64 chunks
+               <= 16384: c2) the RK4 rollout and its sensitivities, 21,996;
       riccati  RK4 sensitivities minus those f evaluations plus the Riccati backward
-               (21,996 - 1,200 + 12,309 = 33,105);
+               (21,996 - 1,200 + 12,309 = 33,105); with the tangent export the Riccati backward
+               alone, 12,309;
       forward  du = K dx + k, dx' = [A|B] (dx, du) (+ gap): 480;
       box      the active-set kernel (c4): per masked backward stage recomputed 12,309 (the Riccati
                algebra over the cached [A|B]), per forward stage 480 + the multipliers
@@ -254,9 +261,13 @@ def phase_kernels(w):
     """
     t = 'float' if w['dtype'] == 'f32' else 'double'
     small = w['batch'] <= 16384
-    # (the rollout-mode instantiations: the mode is a template argument of P1, P2 and P3)
-    names = {'nominal': f'nominal_quad_kernel<{t}, false>' if small else f'nominal_kernel<{t}, false>',
-             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}, false>'}
+    tin = small and w['dtype'] == 'f64'
+    # (the rollout-mode instantiations: the mode is a template argument of P1, P2 and P3; the row
+    # rollout's <T, ITER, DJ, TAN>: DJ = the reference's diagonal inertia)
+    names = {'nominal': f'nominal_row_kernel<{t}, false, true, {"true" if tin else "false"}>' if small
+             else f'nominal_kernel<{t}, false>',
+             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}, false'
+                        + (', true>' if tin else '>')}
     if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
         # (as_kernel_*<true>: the 32-bit stage masks of N <= 32, mpcb_as.hip launch_as)
         names['forward'] = f'as_kernel_{w["dtype"]}<{"true" if w["N"] <= 32 else "false"}, false>'
@@ -267,10 +278,11 @@ def phase_kernels(w):
 
 def kernel_flops(w, r, phase):
     B, N = w['batch'], w['N']
+    tin = B <= 16384 and w['dtype'] == 'f64'
     if phase == 'nominal':
-        return 1200 * N * B
+        return (FLOP_PER_INTERVAL_ROLLOUT_TAN if tin else 1200) * N * B
     if phase == 'riccati':
-        return FLOP_PER_INTERVAL_RICCATI * N * B
+        return (FLOP_PER_INTERVAL_RICCATI_TIN if tin else FLOP_PER_INTERVAL_RICCATI) * N * B
     if w['box']:
         q = r['qp']
         return 12309 * q['bwd_stages'] + (480 + 136) * N * q['fwd_passes']

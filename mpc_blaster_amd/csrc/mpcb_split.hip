@@ -620,6 +620,11 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(2);
     T hj = T(0);
     T G[NZ];
+    double sw[NZ];   // D64: s blkdiag(Q, R) column j, the G accumulators' initial values
+    if constexpr (D64) {
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) sw[i] = SW[i * NZ + j];
+    }
     if constexpr (sizeof(T) == 8 && MPCB_P2_DPP) {
       // Y = P [A|B], h = [A|B]^T pt and G = [A|B]^T Y with row-broadcast FMAs: lane l supplies
       // column l of P (= row l) and pt_l, lane i supplies column i of [A|B]; no LDS operands
@@ -627,9 +632,14 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
       for (int i = 0; i < NX; ++i) y[i] = 0.0;
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) g[i] = 0.0;
+      for (int i = 0; i < NZ; ++i) g[i] = sw[i];   // G = [A|B]^T Y + s blkdiag(Q, R)
       // h = [A|B]^T (p + P gap) = col_j . p + Y_j . gap  (P symmetric)
-      static_for<NX>([&](auto l) { ypn_bc<decltype(l)::value>(y, hj, Pc, pj, col[l]); });
+      ypn_all(y, hj, Pc, pj, col);
+      {   // stage cost of h: (s blkdiag(Q, R) v)_j, v_i = ybar_i - yref_i broadcast from lane i
+        double acc4[4] = {hj, 0.0, 0.0, 0.0};
+        dot16_bc(acc4, cyb - cyr, sw);
+        hj = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+      }
       if (iterate) {
         const T* cc = &Cst[buf][q][0];
 #pragma unroll
@@ -639,12 +649,11 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       // rows of G at the 10 variable directions by broadcasts; the 6 constant ones from Y alone:
       // column e_p of [A|B] gives G[p][j] = Y[p][j], column e_v + hv e_p (hv = the tangent's
       // h/6 * 6) gives G[v][j] = Y[v][j] + hv Y[p][j]
-#pragma unroll
-      for (int l = 0; l < NX; ++l) fmac10_var(g, col[l], y[l]);
+      gvar_all(g, col, y);
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        g[p] = y[p];
-        g[6 + p] = fma(hv, y[p], y[6 + p]);
+        g[p] = y[p] + sw[p];
+        g[6 + p] = fma(hv, y[p], y[6 + p]) + sw[6 + p];
       }
 #else
 #pragma unroll
@@ -686,16 +695,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(3);
     T Huu[NU * NU], hu[NU];
     if constexpr (D64) {
-      // stage cost: G += s blkdiag(Q, R) (lane j: column j), h += (s blkdiag(Q, R) v)_j with v_i
-      // broadcast from lane i; then H_uu and h_u from the input lanes by broadcasts
-      double sw[NZ];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) sw[i] = SW[i * NZ + j];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) G[i] += sw[i];
-      double acc4[4] = {hj, 0.0, 0.0, 0.0};
-      dot16_bc(acc4, cyb - cyr, sw);
-      hj = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+      // (the stage cost is in G's and h's accumulators already) H_uu and h_u from the input lanes
       STAMP(4);
       static_for<NU>([&](auto n) {
         constexpr int nn = decltype(n)::value;
@@ -729,10 +729,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     T Lc[10];
     chol4(Huu, Lc);
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) ok = ok && (Lc[i] == Lc[i]);
-    qp_ok = qp_ok && ok;
+    // every entry of the factor feeds the last pivot (through l30, l31, l32), and inv_sqrt keeps a
+    // NaN: the factor holds a NaN iff its last entry does
+    qp_ok = qp_ok && (Lc[9] == Lc[9]);
     T kff[NU], Kj[NU], nh[NU];
     chol4_solve(Lc, hu, kff);
 #pragma unroll
@@ -747,8 +746,8 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       // Pn[i] = G[i] + sum_m H_ux[m][i] K[m][j]: lane i owns H_ux[:, i] = its G[NX..]
 #pragma unroll
       for (int i = 0; i < NX; ++i) Pn[i] = G[i];
-#pragma unroll
-      for (int m = 0; m < NU; ++m) fmac12_diag(Pn, G[NX + m], Kj[m]);
+      const double gu[NU] = {G[NX], G[NX + 1], G[NX + 2], G[NX + 3]};
+      pn_all(Pn, gu, Kj);
     } else {
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
