@@ -221,8 +221,12 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
     for (int st = 0; st < 4; ++st) {
       // sin/cos of the lane's own state (lanes 3..5: the Euler angles), 1/cos and tan on lane 4
       T S, C;
+#ifdef MPCB_ROW_EXP_NOSC   // timing experiment only (wrong results): sin/cos by two FMAs
+      S = Y; C = fma(T(-0.5) * Y, Y, T(1));
+#else
       if constexpr (sizeof(T) == 8) sc(Y, &S, &C, kc);
       else sc(Y, &S, &C);
+#endif
       const T R = recip(C);
       const T Tn = S * R;
       StageSc<T> c;
@@ -298,7 +302,9 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
       else Xn = fma(h6, XN + F, X);
     }
     if constexpr (TAN) {
-      // column var_col(tv) of [A_k | B_k] into the ABT2 rows: entry (i, tv) at i * ABT2_W + tv
+      // column var_col(tv) of [A_k | B_k] into the ABT2 rows: entry (i, tv) at i * ABT2_W + tv.
+      // (Staging the wave's four records in LDS and writing them as 16-B vectors measured the
+      // same P1 time, 50.3 us at c2, with 75 more instructions per interval.)
       if (exp_lane) {
         T* const abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor) + tv;
 #pragma unroll

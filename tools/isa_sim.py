@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """In-order issue model of one kernel's outermost loop body (one wave alone on its SIMD, the
 situation of the c2 kernels): each instruction issues when the previous one has left the issue
-slot and its source registers are ready.  Costs are the tools/micro/lat_check.hip measurements on
-MI355X (cycles, s_memtime): a dependent v_fma_f64 chain 9.2 per instruction, four independent
-chains 5.3, a DPP row broadcast feeding an FMA ~14, v_rcp_f64 20.  Memory results are taken as
-ready (the loops prefetch a stage ahead).  The estimate ranks schedules of one loop against each
-other; it is not a cycle-accurate model.
+slot and its source registers are ready.  Costs are the tools/micro/issue_check.hip measurements
+on MI355X (cycles, s_memtime at the shader clock): every VALU instruction ~4.4 to issue (fp64,
+fp32, DPP and v_cndmask alike), a dependent fp64 FMA back to back (4.6), a DPP FMA's result after
+7.6, v_rcp_f64 / v_rsq_f64 16 per instruction.  Memory results are taken as ready (the loops
+prefetch a stage ahead).  The estimate ranks schedules of one loop against each other; it is not
+a cycle-accurate model (PMC: the c2 kernels spend ~25 % of their wave cycles in waits it omits).
 
     tools/isa_sim.py FILE.s MANGLED_KERNEL [--trace]
 """
@@ -14,7 +15,7 @@ import sys
 
 sys.path.insert(0, __import__('os').path.dirname(__file__))
 
-ISSUE64, ISSUE32, LAT, LAT_DPP, LAT_TRANS, ISSUE_S = 5.3, 2.0, 9.2, 14.0, 20.0, 1.0
+ISSUE64, ISSUE32, LAT, LAT_DPP, LAT_TRANS, ISSUE_S = 4.4, 4.4, 4.6, 7.6, 20.0, 1.0
 
 
 def loop_body(path, name):
@@ -88,7 +89,7 @@ def simulate(ins, trace=False):
                 lat = LAT_DPP
             if op.startswith(('v_rcp', 'v_rsq', 'v_sqrt', 'v_sin', 'v_cos', 'v_exp', 'v_log')):
                 lat = LAT_TRANS
-                cost = 2 * cost
+                cost = 16.0
         else:
             cost, lat = 1.0, 2.0
         if store or op.startswith(('s_cmp', 'v_cmp')) and False:
