@@ -35,7 +35,7 @@
 #define MPCB_AS_WAVES 2
 #endif
 #ifndef MPCB_AS_FDEPTH   // forward-pass prefetch ring (stages): active-set kernel
-#define MPCB_AS_FDEPTH 1
+#define MPCB_AS_FDEPTH 2
 #endif
 #ifndef MPCB_AS_ITER_T   // the mode as a template argument (as in P1 / P2 / P3)
 #define MPCB_AS_ITER_T 1
@@ -223,6 +223,12 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   };
   bind((int64_t)blockIdx.x * GROUPS + q);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
+  // Every lane issues the same global stores in a backward stage, masked-out ones into this
+  // lane's junk slot: with lane- or group-dependent store counts the compiler's wait for the next
+  // stage's prefetched loads became vmcnt(0), i.e. also for this stage's stores to complete.
+  T* const junk = BOX ? a.junk + (((int64_t)blockIdx.x & (AS_JUNK_WAVES - 1)) * 64 + lane) * AS_JUNK_LANE : nullptr;
+  // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
+  const int cslot = j < 3 ? j : j - 3;
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
   // the stage cost of direction j, when a backward stage needs it
   __shared__ T SW[NZ * NZ];
@@ -325,34 +331,29 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       bool qp_ok = true;
       // stage data one stage ahead: column j of [A|B], own (ybar - yref) and ybar components,
       // own gap component
-      T ncol[NX], ne, nyb, ngp = T(0);
+      // (the prefetch keeps the raw loaded values: forming e = ybar - yref inside it made the
+      // compiler wait for the loads it had just issued, vmcnt(0), at every backward stage)
+      T ncol[NX], nref, nyb, ngp = T(0);
       auto bload = [&](int k) {
-        if (tv >= 0) {
-#if MPCB_AS_AB2
-          ldv<T, NX>(AB.at(k) + tv * NX, ncol);
-#else
-          const T* rows = ABT.at(k) + tv;   // column tv of the stage's ABT2 rows
+        // column tv of the stage's ABT2 rows, or (constant directions) of W.ctab: one load
+        // pattern for every lane (no lane branch: see junk above)
+        const T* rows = tv >= 0 ? ABT.at(k) + tv : W.ctab + cslot;
 #pragma unroll
-          for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
-#endif
-        } else {   // position / velocity directions: e_j, e_j + h e_{j-6}
-#pragma unroll
-          for (int i = 0; i < NX; ++i) ncol[i] = (i == j ? T(1) : T(0)) + ((j >= 6 && i == j - 6) ? h : T(0));
-        }
+        for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
         nyb = XU.at(k)[j * SS];
-        ne = nyb - (stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju]);
-        if (iterate) ngp = stl ? GP.at(k)[jx * SS] : T(0);
+        nref = stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju];
+        if (iterate) ngp = GP.at(k)[jx * SS];   // (input lanes: unused)
       };
-      // (a group loads only the stages it recomputes, k <= kc: the others' results are discarded)
-      if (kmax <= kc) bload(kmax);
+      // (every group loads the wave's stages; one recomputing only k <= kc discards the others)
+      bload(kmax);
       ASTAMP(0);
       for (int k = kmax; k >= 0; --k) {
         const bool act = k <= kc;   // this group's stage is recomputed
         T col[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) col[i] = ncol[i];
-        const T e = ne, yb = nyb, gpo = ngp;
-        if (k > 0 && k - 1 <= kc) bload(k - 1);
+        const T e = nyb - nref, yb = nyb, gpo = ngp;
+        if (k > 0) bload(k - 1);
         // pt = p + P gap (component j), h = [A|B]^T pt
         T pt = pj;
         if (iterate) {
@@ -400,13 +401,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         // unmasked input row of a component fixed at this stage: the forward's multiplier.  (Where
         // the component is free the forward never reads the row, and a stage whose fixed set
         // changes is recomputed -- and its row written -- before the next forward pass.)
-        if (act && valid && !stl && (((lowm | upm) >> k) & 1u)) {
+        {
           T gr[20];
 #pragma unroll
           for (int i = 0; i < NZ; ++i) gr[i] = G[i];
           gr[NZ] = hj;
           gr[17] = gr[18] = gr[19] = T(0);
-          stv<T, 20>(GH.at(k) + ju * 20, gr);
+          const bool wgh = act && valid && !stl && (((lowm | upm) >> k) & 1u);
+          stv<T, 20>(wgh ? GH.at(k) + ju * 20 : junk, gr);
         }
         // the 4x4 input block and h_u from the input lanes; masking of the fixed components
         T Ht[NU * NU], ht[NU], Hux_t[NU];
@@ -470,14 +472,15 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         for (int i = 0; i < NX; ++i) Pn[i] = G[i];
 #pragma unroll
         for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
-        if (act && valid) {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
+        {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12; four stores from every lane, the
+            // masked-out ones (the input lanes' other rows, groups not recomputing this stage) into
+            // the rows' pad slot 13
           T* kr = KR.at(k);
-          if (stl) {
+          const bool w = act && valid;
+          const T kfj = sel<NU>(kff, ju);
 #pragma unroll
-            for (int m = 0; m < NU; ++m) kr[m * KR2_W + j] = Kj[m];
-          } else {
-            kr[ju * KR2_W + 12] = sel<NU>(kff, ju);
-          }
+          for (int m = 0; m < NU; ++m)
+            kr[m * KR2_W + (!w ? 13 : stl ? j : (m == ju ? 12 : 13))] = stl ? Kj[m] : kfj;
         }
         ASTAMP(2);
         // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
@@ -498,7 +501,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         }
         // packed snapshot of P_k, p_k for a later restart: slot d of lane j is P[j][(j + d) % 12],
         // the entry lane max(j, o) published above
-        if (act && valid && stl && k > 0) {
+        {
           T ps[PS2_W];
 #pragma unroll
           for (int d = 0; d < 7; ++d) {
@@ -506,7 +509,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
             ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
           }
           ps[7] = pj;
-          stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);
+          const bool wps = act && valid && stl && k > 0;
+          stv<T, PS2_W>(wps ? PS.at(k) + j * PS2_W : junk + 20, ps);
         }
         wave_lds_sync();
         ASTAMP(3);
@@ -545,15 +549,18 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       if (iterate) pgp[sl] = GP.at(k)[jx * SS];   // state lanes: gap_jx (input lanes: unused)
     };
     auto gload = [&](int k) {
-      if (BOX && (((lowm | upm) >> k) & 1u)) ldv<T, 20>(GH.at(k) + ju * 20, pg);
+      // (the 17 used elements only: loading the row's 3 pad elements too left registers the
+      // compiler reused as temporaries while the load was in flight -- a vmcnt(0) wait per stage)
+      if (BOX && (((lowm | upm) >> k) & 1u)) {
+        ldv<T, 16>(GH.at(k) + ju * 20, pg);
+        pg[NZ] = GH.at(k)[ju * 20 + NZ];
+      }
     };
     // a converged group rides along with its wave's other groups: its loads are skipped and its
     // results (garbage) neither written nor used
     const bool fetch = !BOX || !done;
-    static_for<FD>([&](auto s) {
-      if (decltype(s)::value < N && fetch) rload(decltype(s)::value, s);
-    });
     if (fetch) gload(0);
+    static_for<FD>([&](auto s) { rload(decltype(s)::value < N ? decltype(s)::value : N - 1, s); });
     auto stage = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
       // the lane's row of the dot below: a state lane's row of [A|B] (variable columns loaded,
@@ -626,8 +633,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       } else {
         zj = v;
       }
-      if (k + FD < N && fetch) rload(k + FD, slot_tag);   // refill this slot FD stages ahead
+      // the next stage's Hessian rows (fixed components only), then this slot's refill FD stages
+      // ahead from every lane (the tail reloads stage N - 1, unused): in this order the waits for
+      // both stay exact (see junk above)
       if (k + 1 < N && fetch) gload(k + 1);
+      rload(k + FD < N ? k + FD : N - 1, slot_tag);
       ASTAMP(6);
     };
     for (int k0 = 0; k0 < N; k0 += FD) {

@@ -114,6 +114,14 @@ static void fill_weights(const mpcb_config& c, Weights<T>& w) {
     w.lbu[i] = (T)c.lbu[i];
     w.ubu[i] = (T)c.ubu[i];
   }
+  // constant columns of [A|B] in the ABT2 record layout: slot s <-> direction d = 0,1,2,6,7,8
+  const T hv = ((T)c.dt / T(6)) * T(6);
+  for (int i = 0; i < NX * ABT2_W; ++i) w.ctab[i] = T(0);
+  for (int sl = 0; sl < 6; ++sl) {
+    const int d = sl < 3 ? sl : sl + 3;
+    w.ctab[d * ABT2_W + sl] = T(1);
+    if (d >= 6) w.ctab[(d - 6) * ABT2_W + sl] = hv;
+  }
 }
 
 template <class T>
@@ -247,7 +255,8 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     // the 16-lane row rollout (f split over the lanes, mpcb_rollout.hip) below MPCB_ROW_P1_MAX
     int64_t row_max = 16384;
     if (const char* e = getenv("MPCB_ROW_P1_MAX")) row_max = atoll(e);
-    h->quad_p1 = (chunk <= row_max) ? 2 : (chunk <= quad_max) ? 1 : 0;
+    // (the row rollout stages the wave's u / xbar records in LDS: N <= 120 keeps them <= 64 KiB)
+    h->quad_p1 = (chunk <= row_max && cfg->N <= 120) ? 2 : (chunk <= quad_max) ? 1 : 0;
     // the row rollout also integrates the tangents and exports [A|B] (MPCB_P1_TAN: default on in
     // fp64; in fp32 its regrouped tangent algebra doubled the worst U error of the N=60 box test,
     // 3.7e-5 -> 7.3e-5 against the 5e-5 bound, so fp32 keeps the captured scalars); P2 then reads
@@ -257,8 +266,10 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
-    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
-    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
+    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row; box: the
+    // active-set kernel's junk scratch at the end, SplitArgs::junk)
+    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64 +
+                     (cfg->box_u ? (int64_t)AS_JUNK_WAVES * 64 * AS_JUNK_LANE : 0);
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
   fill_model(*cfg, Jinv, h->Md);
@@ -424,6 +435,7 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.qp_stats = h->qp_stats;
       // the active-set kernel's work counter (MPCB_AS_PERSIST=0: one wave per instance quad)
       a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
+      a.junk = h->cfg.box_u ? base + h->chunk_elems - (int64_t)AS_JUNK_WAVES * 64 * AS_JUNK_LANE : nullptr;
       if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);

@@ -20,6 +20,10 @@ struct Weights {
   T R[NU * NU];
   T QN[NX * NX];
   T lbu[NU], ubu[NU];
+  // the 6 constant columns of [A|B] (position e_p, velocity e_v + hv e_p, hv = the RK4 tangent's
+  // (h/6)*6) laid out like an ABT2 record -- entry i of slot s at i * 10 + s -- so a lane of a
+  // constant direction reads its column with the variable lanes' strided loads (mpcb_as.hip)
+  T ctab[NX * 10];
 };
 
 template <class T>
@@ -88,6 +92,8 @@ constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 //                  in slot 7 (84 slots for its 78 distinct entries); written by P2's unconstrained
 //                  pass and by every stage the active-set kernel recomputes (its restart points)
 constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
+constexpr int AS_JUNK_WAVES = 4096, AS_JUNK_LANE = 32;   // SplitArgs::junk
+static_assert(sizeof(Weights<float>::ctab) == NX * ABT2_W * sizeof(float), "ctab is one ABT2 record");
 // The active-set kernel's backward reads its [A|B] column out of the ABT2 rows (12 strided loads:
 // the masked backward recomputes ~2/3 of the stage-instances once, the forward passes read the
 // rows ~4 times), so P2 writes [A|B] once; MPCB_AS_AB2=1 restores the separate AB2 column export.
@@ -118,6 +124,9 @@ struct SplitArgs {
   int32_t* qp_stats; // box path (nullable): per global instance [forward passes, masked backward
                      // stages] until its active set converged
   int* as_queue;     // box path (nullable): the active-set kernel's work counter
+  T* junk;           // box path: per-lane scratch (AS_JUNK_WAVES x 64 lanes x AS_JUNK_LANE) that
+                     // the active-set kernel's masked-out stores target, so every lane issues the
+                     // same stores and the compiler's waits for prefetched loads stay exact
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

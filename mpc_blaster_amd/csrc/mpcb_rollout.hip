@@ -198,16 +198,37 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   T* const gp0 = ITER ? a.GP + qd * GP_REC * SS + q : nullptr;
   const int64_t xu_k = nq * XU_REC * SS, cc_k = nq * CCS_REC * SS, gp_k = nq * GP_REC * SS;
 
-  const T* xbp = a.xbar + b * (int64_t)(N + 1) * NX;
-  const T* ubp = a.ubar + b * (int64_t)N * NU;
-  const T* ur = a.uref + b * a.uref_sb;
+  // The wave's per-stage inputs (rollout: u_ref; iterate: xbar, ubar) staged in LDS once
+  // (row_lds_elems): a per-interval global load here sat on the chain, and its vmcnt(0) wait
+  // also drained the previous interval's stores -- 24 % of the wave's cycles parked (PMC).
+  extern __shared__ __attribute__((aligned(16))) unsigned char row_dyn[];
+  T* const lu = reinterpret_cast<T*>(row_dyn);          // [GROUPS][N][NU]: u of the stage
+  T* const lx = lu + GROUPS * N * NU;                    // ITER: [GROUPS][N + 1][NX]: xbar
+  {
+    const int nu_e = N * NU, nx_e = (N + 1) * NX;
+    for (int e = lane; e < GROUPS * nu_e; e += 64) {
+      const int g = e / nu_e, r = e - g * nu_e;
+      const int64_t cg = qd * SS + g < nb ? qd * SS + g : nb - 1;
+      lu[e] = ITER ? a.ubar[(a.b0 + cg) * (int64_t)nu_e + r] : a.uref[(a.b0 + cg) * a.uref_sb + r];
+    }
+    if (ITER) {
+      for (int e = lane; e < GROUPS * nx_e; e += 64) {
+        const int g = e / nx_e, r = e - g * nx_e;
+        const int64_t cg = qd * SS + g < nb ? qd * SS + g : nb - 1;
+        lx[e] = a.xbar[(a.b0 + cg) * (int64_t)nx_e + r];
+      }
+    }
+    wave_lds_sync();
+  }
+  const T* const lxq = lx + q * (N + 1) * NX;
+  const T* const luq = lu + q * N * NU;
   // X: x_t (t < 12) / u_{t-12} (t >= 12) of the interval's start
   T X = T(0);
-  if (t < NX) X = ITER ? xbp[t] : a.x0[b * a.x0_sb + t];
+  if (t < NX) X = ITER ? lxq[t] : a.x0[b * a.x0_sb + t];
 
   for (int k = 0; k < N; ++k) {
-    if (ITER && t < NX && k) X = xbp[(int64_t)k * NX + t];
-    if (t >= NX) X = ITER ? ubp[(int64_t)k * NU + (t - NX)] : ur[(int64_t)k * NU + (t - NX)];
+    if (ITER && t < NX && k) X = lxq[k * NX + t];
+    if (t >= NX) X = luq[k * NU + (t - NX)];
     xu0[k * xu_k + t * SS] = X;
     // per-interval constants: the inputs, the thrust scale and J^-1 M(u) + the constant forces
     const T u0 = rbc<12>(X), u1 = rbc<13>(X), u2 = rbc<14>(X), u3 = rbc<15>(X);
@@ -312,33 +333,39 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
       }
     }
     if (ITER) {
-      if (t < NX) gp0[k * gp_k + t * SS] = Xn - xbp[(int64_t)(k + 1) * NX + t];
+      if (t < NX) gp0[k * gp_k + t * SS] = Xn - lxq[(k + 1) * NX + t];
     } else if (t < NX) {
       X = Xn;
     }
   }
   if (t < NX) {
-    if (ITER) X = xbp[(int64_t)N * NX + t];
+    if (ITER) X = lxq[N * NX + t];
   } else {
     X = T(0);
   }
   xu0[N * xu_k + t * SS] = X;
 }
 
+// dynamic LDS of the row rollout: the wave's staged u (and, iterate mode, xbar) records
+template <class T> static size_t row_lds_bytes(const SplitArgs<T>& a) {
+  return (size_t)GROUPS * ((size_t)a.N * NU + (a.mode == MPCB_MODE_ITERATE ? (size_t)(a.N + 1) * NX : 0)) * sizeof(T);
+}
+
 template <class T, bool TAN>
 static void launch_row_m(const SplitArgs<T>& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
+  const size_t lds = row_lds_bytes(a);   // (<= 33 KiB at N = 64, fp64, iterate)
   // diagonal J (and J^-1): the gyroscopic products and their tangent shrink to one term per rate
   bool dj = true;
   for (int i = 0; i < 9; ++i)
     if (i % 4 != 0) dj = dj && a.M.J[i] == T(0) && a.M.Jinv[i] == T(0);
   const bool it = a.mode == MPCB_MODE_ITERATE;
   if (dj) {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true, TAN>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true, TAN>), grid, dim3(64), 0, st, a);
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true, TAN>), grid, dim3(64), lds, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true, TAN>), grid, dim3(64), lds, st, a);
   } else {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false, TAN>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false, TAN>), grid, dim3(64), 0, st, a);
+    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false, TAN>), grid, dim3(64), lds, st, a);
+    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false, TAN>), grid, dim3(64), lds, st, a);
   }
 }
 

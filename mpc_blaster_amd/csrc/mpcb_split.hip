@@ -557,6 +557,17 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     Cst[bufi][q][CCS_REC + j] = pgp;
   };
+  // D64: s blkdiag(Q, R) column j (the G accumulators' initial values) in registers for the
+  // whole recursion: 16 LDS reads and their waits less per stage
+  double sw[NZ];
+  if constexpr (D64) {
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      sw[i] = SW[i * NZ + j];
+      asm volatile("" : "+v"(sw[i]));
+    }
+  }
   prefetch(N - 1);
   commit(0);
   T cyb = pyb, cyr = pyr;
@@ -620,11 +631,6 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(2);
     T hj = T(0);
     T G[NZ];
-    double sw[NZ];   // D64: s blkdiag(Q, R) column j, the G accumulators' initial values
-    if constexpr (D64) {
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) sw[i] = SW[i * NZ + j];
-    }
     if constexpr (sizeof(T) == 8 && MPCB_P2_DPP) {
       // Y = P [A|B], h = [A|B]^T pt and G = [A|B]^T Y with row-broadcast FMAs: lane l supplies
       // column l of P (= row l) and pt_l, lane i supplies column i of [A|B]; no LDS operands
