@@ -223,10 +223,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   };
   bind((int64_t)blockIdx.x * GROUPS + q);
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
-  // Every lane issues the same global stores in a backward stage, masked-out ones into this
-  // lane's junk slot: with lane- or group-dependent store counts the compiler's wait for the next
-  // stage's prefetched loads became vmcnt(0), i.e. also for this stage's stores to complete.
-  T* const junk = BOX ? a.junk + (((int64_t)blockIdx.x & (AS_JUNK_WAVES - 1)) * 64 + lane) * AS_JUNK_LANE : nullptr;
+  // (Measured and dropped, round 4: stores from every lane with the masked-out ones into a
+  // per-lane scratch, so that the waits for the prefetched loads no longer drain the stores --
+  // 3.15 -> 4.73 ms, the scratch writes cost more than the drains; prefetching the backward
+  // stages for every group: no change.)
   // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
   const int cslot = j < 3 ? j : j - 3;
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
@@ -336,7 +336,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       T ncol[NX], nref, nyb, ngp = T(0);
       auto bload = [&](int k) {
         // column tv of the stage's ABT2 rows, or (constant directions) of W.ctab: one load
-        // pattern for every lane (no lane branch: see junk above)
+        // pattern for every lane (no lane branch)
         const T* rows = tv >= 0 ? ABT.at(k) + tv : W.ctab + cslot;
 #pragma unroll
         for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
@@ -344,8 +344,8 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         nref = stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju];
         if (iterate) ngp = GP.at(k)[jx * SS];   // (input lanes: unused)
       };
-      // (every group loads the wave's stages; one recomputing only k <= kc discards the others)
-      bload(kmax);
+      // (a group loads only the stages it recomputes, k <= kc: the others' results are discarded)
+      if (kmax <= kc) bload(kmax);
       ASTAMP(0);
       for (int k = kmax; k >= 0; --k) {
         const bool act = k <= kc;   // this group's stage is recomputed
@@ -353,7 +353,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) col[i] = ncol[i];
         const T e = nyb - nref, yb = nyb, gpo = ngp;
-        if (k > 0) bload(k - 1);
+        if (k > 0 && k - 1 <= kc) bload(k - 1);
         // pt = p + P gap (component j), h = [A|B]^T pt
         T pt = pj;
         if (iterate) {
@@ -407,8 +407,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           for (int i = 0; i < NZ; ++i) gr[i] = G[i];
           gr[NZ] = hj;
           gr[17] = gr[18] = gr[19] = T(0);
-          const bool wgh = act && valid && !stl && (((lowm | upm) >> k) & 1u);
-          stv<T, 20>(wgh ? GH.at(k) + ju * 20 : junk, gr);
+          if (act && valid && !stl && (((lowm | upm) >> k) & 1u)) stv<T, 20>(GH.at(k) + ju * 20, gr);
         }
         // the 4x4 input block and h_u from the input lanes; masking of the fixed components
         T Ht[NU * NU], ht[NU], Hux_t[NU];
@@ -472,15 +471,16 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         for (int i = 0; i < NX; ++i) Pn[i] = G[i];
 #pragma unroll
         for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
-        {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12; four stores from every lane, the
-            // masked-out ones (the input lanes' other rows, groups not recomputing this stage) into
-            // the rows' pad slot 13
-          T* kr = KR.at(k);
-          const bool w = act && valid;
-          const T kfj = sel<NU>(kff, ju);
+        {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
+          if (act && valid) {
+            T* kr = KR.at(k);
+            if (stl) {
 #pragma unroll
-          for (int m = 0; m < NU; ++m)
-            kr[m * KR2_W + (!w ? 13 : stl ? j : (m == ju ? 12 : 13))] = stl ? Kj[m] : kfj;
+              for (int m = 0; m < NU; ++m) kr[m * KR2_W + j] = Kj[m];
+            } else {
+              kr[ju * KR2_W + 12] = sel<NU>(kff, ju);
+            }
+          }
         }
         ASTAMP(2);
         // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
@@ -509,8 +509,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
             ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
           }
           ps[7] = pj;
-          const bool wps = act && valid && stl && k > 0;
-          stv<T, PS2_W>(wps ? PS.at(k) + j * PS2_W : junk + 20, ps);
+          if (act && valid && stl && k > 0) stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);
         }
         wave_lds_sync();
         ASTAMP(3);
@@ -635,7 +634,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       }
       // the next stage's Hessian rows (fixed components only), then this slot's refill FD stages
       // ahead from every lane (the tail reloads stage N - 1, unused): in this order the waits for
-      // both stay exact (see junk above)
+      // both stay exact
       if (k + 1 < N && fetch) gload(k + 1);
       rload(k + FD < N ? k + FD : N - 1, slot_tag);
       ASTAMP(6);

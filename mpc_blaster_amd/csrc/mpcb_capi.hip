@@ -266,10 +266,8 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);
-    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row; box: the
-    // active-set kernel's junk scratch at the end, SplitArgs::junk)
-    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64 +
-                     (cfg->box_u ? (int64_t)AS_JUNK_WAVES * 64 * AS_JUNK_LANE : 0);
+    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
+    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
   }
   fill_model(*cfg, Jinv, h->Md);
@@ -435,7 +433,6 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.qp_stats = h->qp_stats;
       // the active-set kernel's work counter (MPCB_AS_PERSIST=0: one wave per instance quad)
       a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
-      a.junk = h->cfg.box_u ? base + h->chunk_elems - (int64_t)AS_JUNK_WAVES * 64 * AS_JUNK_LANE : nullptr;
       if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);

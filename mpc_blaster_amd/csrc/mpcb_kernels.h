@@ -92,7 +92,6 @@ constexpr int AB_REC = 12 * NVAR, GH_REC = 4 * 17, PS_REC = 12 * 13;
 //                  in slot 7 (84 slots for its 78 distinct entries); written by P2's unconstrained
 //                  pass and by every stage the active-set kernel recomputes (its restart points)
 constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
-constexpr int AS_JUNK_WAVES = 4096, AS_JUNK_LANE = 32;   // SplitArgs::junk
 static_assert(sizeof(Weights<float>::ctab) == NX * ABT2_W * sizeof(float), "ctab is one ABT2 record");
 // The active-set kernel's backward reads its [A|B] column out of the ABT2 rows (12 strided loads:
 // the masked backward recomputes ~2/3 of the stage-instances once, the forward passes read the
@@ -124,9 +123,6 @@ struct SplitArgs {
   int32_t* qp_stats; // box path (nullable): per global instance [forward passes, masked backward
                      // stages] until its active set converged
   int* as_queue;     // box path (nullable): the active-set kernel's work counter
-  T* junk;           // box path: per-lane scratch (AS_JUNK_WAVES x 64 lanes x AS_JUNK_LANE) that
-                     // the active-set kernel's masked-out stores target, so every lane issues the
-                     // same stores and the compiler's waits for prefetched loads stay exact
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

@@ -537,6 +537,9 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   for (int i = 0; i < NX; ++i)
     ce[i] = (tvj >= 0) ? T(0) : ((i == j) ? T(1) : (j >= 6 && j < 9 && i == j - 6) ? hv : T(0));
   auto prefetch = [&](int k) {
+#ifdef MPCB_P2_EXP_FIXLOAD   // timing experiment only (wrong results): every stage loads stage N - 1
+    k = N - 1;
+#endif
     if constexpr (TIN) {
       const T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor) + (tvj >= 0 ? tvj : 0);
 #pragma unroll
