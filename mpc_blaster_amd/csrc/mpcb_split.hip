@@ -449,6 +449,12 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
 #ifndef MPCB_P2_MVGPR
 #define MPCB_P2_MVGPR 1
 #endif
+#ifndef MPCB_P2_R32
+#define MPCB_P2_R32 1
+#endif
+template <int L> __device__ __forceinline__ float rbc32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xF, 0xF, false));
+}
 // TIN: the row rollout already integrated the tangents (SplitArgs::tin): column j of [A|B] comes
 // from its ABT2 rows (variable directions) or is the constant e_j / e_j + hv e_{j-6} (the others),
 // prefetched one stage ahead like the captured scalars it replaces
@@ -464,6 +470,13 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   // the stage-cost term S v, H_uu and h_u by broadcasts -- so P needs no LDS transpose and the
   // stage no LDS round trip (the box path's snapshots still publish P through LDS)
   constexpr bool D64 = sizeof(T) == 8 && MPCB_P2_DPP;
+  // fp32 (MFMA products), export instantiation: the stage cost, h, the input block and the P update
+  // by row broadcasts too (MPCB_P2_R32, default on; P's symmetric exchange stays in LDS).  Measured:
+  // c4 P2 1.04 -> 1.02-1.03 ms; in the export-free instantiation (c3, c5: two or more waves per
+  // SIMD) the broadcasts cost more issue than the LDS exchanges they replace (c3 0.51 -> 0.54 ms,
+  // c5 1.86 -> 1.97 ms), so it keeps LDS
+  constexpr bool R32 = sizeof(T) == 4 && EXPORT && MPCB_P2_R32;
+  constexpr bool DREG = D64 || R32;
   __shared__ GroupLds<T> lds_all[GROUPS];
   const int lane = threadIdx.x;
   const int q = lane >> 4;
@@ -562,8 +575,8 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   };
   // D64: s blkdiag(Q, R) column j (the G accumulators' initial values) in registers for the
   // whole recursion: 16 LDS reads and their waits less per stage
-  double sw[NZ];
-  if constexpr (D64) {
+  T sw[NZ];
+  if constexpr (DREG) {
     wave_lds_sync();
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
@@ -579,6 +592,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   STAMP_INIT();
   for (int k = N - 1; k >= 0; --k) {
     T col[NX];
+    T ptr = T(0);   // R32: this lane's entry of p + P gap
     if constexpr (TIN) {
 #pragma unroll
       for (int i = 0; i < NX; ++i) col[i] = fma(kvar, pc[i], ce[i]);
@@ -587,7 +601,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(0);
     {
       const T* cc = &Cst[buf][q][0];
-      if constexpr (!D64) L.v[j] = cyb - cyr;
+      if constexpr (!DREG) L.v[j] = cyb - cyr;
       if constexpr (!TIN) {
         T dx[NX], du[NU];
 #pragma unroll
@@ -623,7 +637,8 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
           for (int i = 0; i < NX; ++i) pt += Pc[i] * cc[CCS_REC + i];
         }
-        L.hv[j] = pt;
+        if constexpr (R32) ptr = pt;
+        else L.hv[j] = pt;
       }
     }
     if constexpr (sizeof(T) == 8 && !MPCB_P2_DPP) {   // LDS-operand fp64 products
@@ -670,6 +685,12 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #endif
 #pragma unroll
       for (int i = 0; i < NZ; ++i) G[i] = g[i];
+    } else if constexpr (R32) {
+      // h = [A|B]^T pt with pt_l broadcast from lane l, plus the stage cost's (S v)_j
+      T acc4[4] = {T(0), T(0), T(0), T(0)};
+      dot12_bc(acc4, ptr, col);
+      dot16_bc(acc4, cyb - cyr, sw);
+      hj = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
     } else {
 #pragma unroll
     for (int l = 0; l < NX; ++l) hj += col[l] * L.hv[l];
@@ -680,7 +701,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       to_columns(outer12(Pc, col), y);     // lane (q,j): Y_q[:, j]  (P symmetric: row = column)
       to_columns(outer12(col, y), g);      // lane (q,j): G_q[:, j]
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) G[i] = g[i];
+      for (int i = 0; i < NZ; ++i) G[i] = R32 ? g[i] + sw[i] : g[i];
     } else if constexpr (!MPCB_P2_DPP) {
       // (measured: v_mfma_f64_16x16x4_f64 for Y and G with an LDS transpose cut this section
       // from 5.6k to 3.8k cycles per stage but cost more elsewhere, 14.6k vs 13.7k in total)
@@ -703,14 +724,18 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     }
     STAMP(3);
     T Huu[NU * NU], hu[NU];
-    if constexpr (D64) {
+    if constexpr (DREG) {
       // (the stage cost is in G's and h's accumulators already) H_uu and h_u from the input lanes
       STAMP(4);
       static_for<NU>([&](auto n) {
         constexpr int nn = decltype(n)::value;
 #pragma unroll
-        for (int m = 0; m < NU; ++m) Huu[m * NU + nn] = rbc64<NX + nn>(G[NX + m]);
-        hu[nn] = -rbc64<NX + nn>(hj);
+        for (int m = 0; m < NU; ++m) {
+          if constexpr (D64) Huu[m * NU + nn] = rbc64<NX + nn>(G[NX + m]);
+          else Huu[m * NU + nn] = rbc32<NX + nn>(G[NX + m]);
+        }
+        if constexpr (D64) hu[nn] = -rbc64<NX + nn>(hj);
+        else hu[nn] = -rbc32<NX + nn>(hj);
       });
     } else {
 #pragma unroll
@@ -751,11 +776,11 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
 #pragma unroll
     for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
     T Pn[NX];
-    if constexpr (sizeof(T) == 8 && MPCB_P2_DPP) {
+    if constexpr (DREG) {
       // Pn[i] = G[i] + sum_m H_ux[m][i] K[m][j]: lane i owns H_ux[:, i] = its G[NX..]
 #pragma unroll
       for (int i = 0; i < NX; ++i) Pn[i] = G[i];
-      const double gu[NU] = {G[NX], G[NX + 1], G[NX + 2], G[NX + 3]};
+      const T gu[NU] = {G[NX], G[NX + 1], G[NX + 2], G[NX + 3]};
       pn_all(Pn, gu, Kj);
     } else {
 #pragma unroll
