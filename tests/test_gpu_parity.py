@@ -538,3 +538,58 @@ def test_box_long_horizon_w64_matches_oracle(dtype, mode):
     print(f'box N={N} {dtype} {mode}: max rel err u0 {e_u.max():.2e} U {e_U.max():.2e} X {e_x.max():.2e}')
     assert e_u.max() < tol and e_U.max() < tol and e_x.max() < tol
     assert (U >= -1e-5).all() and (U <= 65 + 1e-4).all()
+
+
+_J_GENERAL = np.array([[0.50781, 0.012, -0.008], [0.012, 0.47314, 0.015], [-0.008, 0.015, 0.72975]])
+
+
+@pytest.mark.parametrize('dtype,mode', [('f64', 'rollout'), ('f64', 'iterate'), ('f32', 'rollout')])
+def test_row_rollout_general_inertia_matches_oracle(dtype, mode):
+    """The 16-lane row rollout (chunks <= 16384, mpcb_rollout.hip) with a NON-diagonal inertia:
+    the general quadratic form of w x Jw and, in fp64, the general tangent of the exported
+    [A|B] (template DJ = false; the reference's diagonal J takes DJ = true everywhere else), at
+    an odd horizon and a ragged batch, against the oracle with the same J."""
+    from oracle.model import Params
+    N, B = 13, 37
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    spec = OcpSpec(N=N, params=Params(J=_J_GENERAL))
+    m = _mpc(N, dtype, max_batch=B, path='split', J=_J_GENERAL)
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    if mode == 'iterate':
+        rng = np.random.default_rng(13)
+        xbar = inp['xref'] + rng.normal(scale=0.05, size=(B, N + 1, 12))
+        ubar = inp['uref'] + rng.normal(scale=1.0, size=(B, N, 4))
+        m.solve_iterate(inp['x0'], xbar, ubar, inp['xref'], inp['uref'])
+        o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], spec, mode='iterate', xbar=xbar, ubar=ubar)
+    else:
+        m.solve(inp['x0'], inp['xref'], inp['uref'])
+        o = mpc_solve(cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), spec)
+    torch.cuda.synchronize()
+    tol = 1e-9 if dtype == 'f64' else 5e-5
+    e_u = relerr(m.get_control().cpu().numpy(), o['u0'])
+    e_x = relerr(m.get_state_trajectory().cpu().numpy(), o['X'])
+    e_U = relerr(m.get_input_trajectory().cpu().numpy(), o['U'])
+    print(f'general J {dtype} {mode}: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
+    assert (m.get_status().cpu().numpy() == 0).all()
+    assert e_u.max() < tol and e_x.max() < tol and e_U.max() < tol
+
+
+@pytest.mark.parametrize('N', [20, 7])
+def test_rollout_tangent_export_equals_captured_scalar_path(N):
+    """fp64 small chunks: the rollout that integrates the sensitivities and exports [A|B]
+    (SplitArgs::tin, the default) against the round-3 split whose P2 integrates them from the
+    captured scalars (MPCB_P1_TAN=0): the same solve to rounding, both modes."""
+    B = 61
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    res = []
+    for tan in ('1', '0'):
+        os.environ['MPCB_P1_TAN'] = tan
+        try:
+            m = _mpc(N, 'f64', max_batch=B, path='split')
+        finally:
+            os.environ.pop('MPCB_P1_TAN')
+        m.solve(inp['x0'], inp['xref'], inp['uref'])
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in (m.get_control(), m.get_state_trajectory(), m.get_input_trajectory())])
+    for a, b in zip(*res):
+        assert relerr(a, b).max() < 1e-12
