@@ -450,7 +450,7 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
 #define MPCB_P2_MVGPR 1
 #endif
 #ifndef MPCB_P2_R32
-#define MPCB_P2_R32 1
+#define MPCB_P2_R32 0
 #endif
 template <int L> __device__ __forceinline__ float rbc32(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xF, 0xF, false));
@@ -471,10 +471,11 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   // stage no LDS round trip (the box path's snapshots still publish P through LDS)
   constexpr bool D64 = sizeof(T) == 8 && MPCB_P2_DPP;
   // fp32 (MFMA products), export instantiation: the stage cost, h, the input block and the P update
-  // by row broadcasts too (MPCB_P2_R32, default on; P's symmetric exchange stays in LDS).  Measured:
-  // c4 P2 1.04 -> 1.02-1.03 ms; in the export-free instantiation (c3, c5: two or more waves per
-  // SIMD) the broadcasts cost more issue than the LDS exchanges they replace (c3 0.51 -> 0.54 ms,
-  // c5 1.86 -> 1.97 ms), so it keeps LDS
+  // by row broadcasts too (MPCB_P2_R32; P's symmetric exchange stays in LDS).  Measured: c4 P2
+  // 1.04 -> 1.02-1.03 ms; in the export-free instantiation (c3, c5: two or more waves per SIMD) the
+  // broadcasts cost more issue than the LDS exchanges they replace (c3 0.51 -> 0.54 ms, c5 1.86 ->
+  // 1.97 ms).  Off by default: in the export instantiation alone it changes the summation order,
+  // so u0 would differ in the last bit between want_traj = 0 and 1 (test_u0_only_path_equals_full_path)
   constexpr bool R32 = sizeof(T) == 4 && EXPORT && MPCB_P2_R32;
   constexpr bool DREG = D64 || R32;
   __shared__ GroupLds<T> lds_all[GROUPS];
