@@ -23,6 +23,8 @@
 // P2 is unchanged; likewise XU (x_k, u_k) and, in iterate mode, the gaps GP.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/mpcb.h"
 #include "mpcb_common.h"
 #include "mpcb_kernels.h"
@@ -41,8 +43,26 @@ template <class T> __device__ __forceinline__ T shl6(T v) {
   return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true);
 }
 
-template <class T> struct ScOf { using type = ScConst; };
-template <> struct ScOf<double> { using type = ScRegs; };
+// Taylor coefficients of the stage angle offsets (MPCB_ROW_SC_ADD) as opaque loop-invariant
+// registers (fp64 constants are not encodable as literals): sin d = d + d^3 (v0 d^6 + v1 d^4 +
+// v2 d^2 + v3), cos d - 1 = d^2 (v4 d^8 + v5 d^6 + v6 d^4 + v7 d^2 + v8)
+#ifndef MPCB_ROW_SC_ADD
+#define MPCB_ROW_SC_ADD 1
+#endif
+struct SaRegs {
+  double v[9];
+  __device__ __forceinline__ SaRegs() {
+    v[0] = 1.0 / 362880.0; v[1] = -1.0 / 5040.0; v[2] = 1.0 / 120.0; v[3] = -1.0 / 6.0;
+    v[4] = -1.0 / 3628800.0; v[5] = 1.0 / 40320.0; v[6] = -1.0 / 720.0; v[7] = 1.0 / 24.0; v[8] = -0.5;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(v[i]));
+  }
+};
+
+struct SaNone {};
+
+template <class T> struct ScOf { using type = ScConst; using sa = SaNone; };
+template <> struct ScOf<double> { using type = ScRegs; using sa = std::conditional_t<MPCB_ROW_SC_ADD != 0, SaRegs, SaNone>; };
 
 }  // namespace
 
@@ -169,6 +189,7 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   if (a.wind && t >= 6 && t < 9) K0 = a.wind[b * a.wind_sb + (t - 6)] * M.minv;
   if (t == 8) K0 -= M.g;
   const typename ScOf<T>::type kc;
+  const typename ScOf<T>::sa sa;
   // the tangent's lane constants (TAN): direction e_t; its input part e_{t-12} on lanes 12..15
   TanConst<T> K{};
   T ev[NX];
@@ -235,6 +256,7 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
     const T s = ((u0 + u1) + (u2 + u3) + M.t_blast) * M.minv;
     const T Kt = fma(Lm[0], u0, fma(Lm[1], u1, fma(Lm[2], u2, fma(Lm[3], u3, K0))));
     T Y = X, XN = T(0), Xn = T(0);
+    T S0 = T(0), C0 = T(1);   // sin / cos of the interval start (MPCB_ROW_SC_ADD)
     T dS[NX], dN[NX];   // TAN: the stage's tangent input and the RK4 accumulator
 #pragma unroll
     for (int i = 0; i < NX; ++i) dS[i] = ev[i];
@@ -245,8 +267,37 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
 #ifdef MPCB_ROW_EXP_NOSC   // timing experiment only (wrong results): sin/cos by two FMAs
       S = Y; C = fma(T(-0.5) * Y, Y, T(1));
 #else
-      if constexpr (sizeof(T) == 8) sc(Y, &S, &C, kc);
-      else sc(Y, &S, &C);
+      if constexpr (sizeof(T) == 8 && MPCB_ROW_SC_ADD) {
+        // stages 1..3 by angle addition from the interval start's sin/cos (Y = X + c h k): the
+        // stage offset d = Y - X is small, so sin d and cos d - 1 are short Taylor series (|d| <=
+        // 1/8: truncation below 2e-17 relative); a wave with a larger angle offset takes sc()
+        if (st == 0) {
+          sc(Y, &S, &C, kc);
+          S0 = S; C0 = C;
+        } else {
+          const T d = Y - X;
+          if (__any(t >= 3 && t < 6 && !(fabs(d) <= T(0.125)))) {
+            sc(Y, &S, &C, kc);
+          } else {
+            const T d2 = d * d;
+            T ps = hstep(sa.v[0], d2, sa.v[1]);
+            ps = hstep(ps, d2, sa.v[2]);
+            ps = hstep(ps, d2, sa.v[3]);
+            const T sd = fma(d * d2, ps, d);                    // sin d
+            T pc = hstep(sa.v[4], d2, sa.v[5]);
+            pc = hstep(pc, d2, sa.v[6]);
+            pc = hstep(pc, d2, sa.v[7]);
+            pc = hstep(pc, d2, sa.v[8]);
+            const T cm = d2 * pc;                               // cos d - 1
+            S = S0 + fma(S0, cm, C0 * sd);
+            C = C0 + fma(C0, cm, -(S0 * sd));
+          }
+        }
+      } else if constexpr (sizeof(T) == 8) {
+        sc(Y, &S, &C, kc);
+      } else {
+        sc(Y, &S, &C);
+      }
 #endif
       const T R = recip(C);
       const T Tn = S * R;
