@@ -81,11 +81,9 @@ struct ScRegs {
 #ifndef MPCB_SC_FALLBACK
 #define MPCB_SC_FALLBACK 1
 #endif
+// sc_core: the reduction and kernels alone, valid for |a| < 2^19 (the caller checks the domain)
 template <class K>
-__device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
-#if MPCB_SC_FALLBACK
-  if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
-#endif
+__device__ __forceinline__ void sc_core(double a, double* s, double* c, const K& k) {
   const double n = rint(a * 6.36619772367581382433e-01);           // 2/pi
   double r = fma(-n, 1.57079632673412561417e+00, a);              // pio2_1 (33 bits)
   r = fma(-n, 6.07710050650619224932e-11, r);                     // pio2_1t
@@ -110,11 +108,16 @@ __device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
   *s = (q & 2) ? -s0 : s0;
   *c = ((q + 1) & 2) ? -c0 : c0;
 }
-__device__ __forceinline__ void sc(double a, double* s, double* c) { sc(a, s, c, ScConst{}); }
-__device__ __forceinline__ void sc(float a, float* s, float* c) {
+template <class K>
+__device__ __forceinline__ void sc(double a, double* s, double* c, const K& k) {
 #if MPCB_SC_FALLBACK
-  if (!(fabsf(a) < 8192.0f)) { sincosf(a, s, c); return; }
+  if (!(fabs(a) < 524288.0)) { sincos(a, s, c); return; }
 #endif
+  sc_core(a, s, c, k);
+}
+__device__ __forceinline__ void sc(double a, double* s, double* c) { sc(a, s, c, ScConst{}); }
+// fp32: |a| < 8192
+__device__ __forceinline__ void sc_core(float a, float* s, float* c) {
   const float n = rintf(a * 0.636619772367581343f);
   float r = fmaf(-n, 1.57079637050628662109375f, a);              // pio2 hi
   r = fmaf(-n, -4.37113900018624283e-08f, r);                     // pio2 lo
@@ -126,6 +129,12 @@ __device__ __forceinline__ void sc(float a, float* s, float* c) {
   const float s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
   *s = (q & 2) ? -s0 : s0;
   *c = ((q + 1) & 2) ? -c0 : c0;
+}
+__device__ __forceinline__ void sc(float a, float* s, float* c) {
+#if MPCB_SC_FALLBACK
+  if (!(fabsf(a) < 8192.0f)) { sincosf(a, s, c); return; }
+#endif
+  sc_core(a, s, c);
 }
 
 // 1/x by the hardware reciprocal and two Newton steps (fp64: v_rcp_f64 + 4 FMAs, ~1 ulp; the

@@ -255,30 +255,42 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
     const T u0 = rbc<12>(X), u1 = rbc<13>(X), u2 = rbc<14>(X), u3 = rbc<15>(X);
     const T s = ((u0 + u1) + (u2 + u3) + M.t_blast) * M.minv;
     const T Kt = fma(Lm[0], u0, fma(Lm[1], u1, fma(Lm[2], u2, fma(Lm[3], u3, K0))));
-    T Y = X, XN = T(0), Xn = T(0);
-    T S0 = T(0), C0 = T(1);   // sin / cos of the interval start (MPCB_ROW_SC_ADD)
-    T dS[NX], dN[NX];   // TAN: the stage's tangent input and the RK4 accumulator
+    T Xn = T(0);
+    T dN[NX];   // TAN: the RK4 tangent accumulator
+    // One interval.  SLOW = false: sin/cos without their range fallbacks (sc_core at stage 0,
+    // angle addition at stages 1..3), so the four stages are one basic block in which the
+    // scheduler interleaves the tangent of stage s with the sin/cos of stage s + 1 (a branch per
+    // stage around the fallbacks kept them apart: P1 45 -> 39 us at c2).  It returns whether an
+    // angle lane was outside those ranges; the wave then recomputes the interval with SLOW = true
+    // (sc() and its fallback at every stage) before anything of the interval but the CC record,
+    // which the second pass rewrites, is stored.
+    auto interval = [&](auto slow_tag) -> bool {
+      constexpr bool SLOW = decltype(slow_tag)::value;
+      bool bad = false;
+      T Y = X, XN = T(0);
+      T S0 = T(0), C0 = T(1);   // sin / cos of the interval start (MPCB_ROW_SC_ADD)
+      T dS[NX];   // TAN: the stage's tangent input
 #pragma unroll
-    for (int i = 0; i < NX; ++i) dS[i] = ev[i];
+      for (int i = 0; i < NX; ++i) dS[i] = ev[i];
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      // sin/cos of the lane's own state (lanes 3..5: the Euler angles), 1/cos and tan on lane 4
-      T S, C;
-#ifdef MPCB_ROW_EXP_NOSC   // timing experiment only (wrong results): sin/cos by two FMAs
-      S = Y; C = fma(T(-0.5) * Y, Y, T(1));
-#else
-      if constexpr (sizeof(T) == 8 && MPCB_ROW_SC_ADD) {
-        // stages 1..3 by angle addition from the interval start's sin/cos (Y = X + c h k): the
-        // stage offset d = Y - X is small, so sin d and cos d - 1 are short Taylor series (|d| <=
-        // 1/8: truncation below 2e-17 relative); a wave with a larger angle offset takes sc()
-        if (st == 0) {
-          sc(Y, &S, &C, kc);
-          S0 = S; C0 = C;
-        } else {
-          const T d = Y - X;
-          if (__any(t >= 3 && t < 6 && !(fabs(d) <= T(0.125)))) {
-            sc(Y, &S, &C, kc);
+      for (int st = 0; st < 4; ++st) {
+        // sin/cos of the lane's own state (lanes 3..5: the Euler angles), 1/cos and tan on lane 4
+        T S, C;
+        const bool ang = t >= 3 && t < 6;   // the Euler-angle lanes: the only sin/cos used
+        if constexpr (SLOW) {
+          if constexpr (sizeof(T) == 8) sc(Y, &S, &C, kc);
+          else sc(Y, &S, &C);
+        } else if constexpr (sizeof(T) == 8 && MPCB_ROW_SC_ADD) {
+          // stages 1..3 by angle addition from the interval start's sin/cos (Y = X + c h k): the
+          // stage offset d = Y - X is small, so sin d and cos d - 1 are short Taylor series (|d| <=
+          // 1/8: truncation below 2e-17 relative)
+          if (st == 0) {
+            sc_core(Y, &S, &C, kc);
+            bad = bad || (ang && !(fabs(Y) < 524288.0));
+            S0 = S; C0 = C;
           } else {
+            const T d = Y - X;
+            bad = bad || (ang && !(fabs(d) <= T(0.125)));
             const T d2 = d * d;
             T ps = hstep(sa.v[0], d2, sa.v[1]);
             ps = hstep(ps, d2, sa.v[2]);
@@ -292,87 +304,99 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
             S = S0 + fma(S0, cm, C0 * sd);
             C = C0 + fma(C0, cm, -(S0 * sd));
           }
+        } else if constexpr (sizeof(T) == 8) {
+          sc_core(Y, &S, &C, kc);
+          bad = bad || (ang && !(fabs(Y) < 524288.0));
+        } else {
+          sc_core(Y, &S, &C);
+          bad = bad || (ang && !(fabsf(Y) < 8192.0f));
         }
-      } else if constexpr (sizeof(T) == 8) {
-        sc(Y, &S, &C, kc);
-      } else {
-        sc(Y, &S, &C);
-      }
-#endif
-      const T R = recip(C);
-      const T Tn = S * R;
-      StageSc<T> c;
-      c.sf = rbc<3>(S); c.cf = rbc<3>(C); c.st = rbc<4>(S); c.ct = rbc<4>(C);
-      c.sp = rbc<5>(S); c.cp = rbc<5>(C); c.ict = rbc<4>(R); c.tt = rbc<4>(Tn);
-      c.wx = rbc<9>(Y); c.wy = rbc<10>(Y); c.wz = rbc<11>(Y);
-      c.a = c.sf * c.wy + c.cf * c.wz;
-      c.b = c.cf * c.wy - c.sf * c.wz;
-      c.cfst = c.cf * c.st;
-      c.r0 = c.cp * c.cfst + c.sp * c.sf;
-      c.r1 = c.sp * c.cfst - c.cp * c.sf;
-      c.r2 = c.cf * c.ct;
-      c.s = s;
-      // lane t's row of f, as three independent partial sums
-      T F0 = fma(kv, shl6(Y), Kt);
-      T F1 = fma(k4, c.b, k1 * c.wx);
-      T F2 = c.s * fma(kr0, c.r0, fma(kr1, c.r1, kr2 * c.r2));
-      F0 = fma(c.a, fma(k2, c.tt, k3 * c.ict), F0);
-      if constexpr (DJ) {
-        F1 = fma(G[5], c.wy * c.wz, F1);
-        F2 = fma(G[4], c.wx * c.wz, F2);
-        F0 = fma(G[3], c.wx * c.wy, F0);
-      } else {
-        F1 = fma(G[0], c.wx * c.wx, F1);
-        F2 = fma(G[1], c.wy * c.wy, F2);
-        F0 = fma(G[2], c.wz * c.wz, F0);
-        F1 = fma(G[3], c.wx * c.wy, F1);
-        F2 = fma(G[4], c.wx * c.wz, F2);
-        F0 = fma(G[5], c.wy * c.wz, F0);
-      }
-      const T F = F0 + (F1 + F2);
-      const T JW = fma(J0, c.wx, fma(J1, c.wy, J2 * c.wz));
-      if constexpr (TAN) {
-        if constexpr (!DJ) { c.jw0 = rbc<9>(JW); c.jw1 = rbc<10>(JW); c.jw2 = rbc<11>(JW); }
-        T dk[NX];
-        tan_stage<T, DJ>(c, dS, K, dk);
-        // RK4 tangent update (mpcb_model.h rk4_tan: same operations)
+        const T R = recip(C);
+        const T Tn = S * R;
+        StageSc<T> c;
+        c.sf = rbc<3>(S); c.cf = rbc<3>(C); c.st = rbc<4>(S); c.ct = rbc<4>(C);
+        c.sp = rbc<5>(S); c.cp = rbc<5>(C); c.ict = rbc<4>(R); c.tt = rbc<4>(Tn);
+        c.wx = rbc<9>(Y); c.wy = rbc<10>(Y); c.wz = rbc<11>(Y);
+        c.a = c.sf * c.wy + c.cf * c.wz;
+        c.b = c.cf * c.wy - c.sf * c.wz;
+        c.cfst = c.cf * c.st;
+        c.r0 = c.cp * c.cfst + c.sp * c.sf;
+        c.r1 = c.sp * c.cfst - c.cp * c.sf;
+        c.r2 = c.cf * c.ct;
+        c.s = s;
+        // lane t's row of f, as three independent partial sums
+        T F0 = fma(kv, shl6(Y), Kt);
+        T F1 = fma(k4, c.b, k1 * c.wx);
+        T F2 = c.s * fma(kr0, c.r0, fma(kr1, c.r1, kr2 * c.r2));
+        F0 = fma(c.a, fma(k2, c.tt, k3 * c.ict), F0);
+        if constexpr (DJ) {
+          F1 = fma(G[5], c.wy * c.wz, F1);
+          F2 = fma(G[4], c.wx * c.wz, F2);
+          F0 = fma(G[3], c.wx * c.wy, F0);
+        } else {
+          F1 = fma(G[0], c.wx * c.wx, F1);
+          F2 = fma(G[1], c.wy * c.wy, F2);
+          F0 = fma(G[2], c.wz * c.wz, F0);
+          F1 = fma(G[3], c.wx * c.wy, F1);
+          F2 = fma(G[4], c.wx * c.wz, F2);
+          F0 = fma(G[5], c.wy * c.wz, F0);
+        }
+        const T F = F0 + (F1 + F2);
+        const T JW = fma(J0, c.wx, fma(J1, c.wy, J2 * c.wz));
+        if constexpr (TAN) {
+          if constexpr (!DJ) { c.jw0 = rbc<9>(JW); c.jw1 = rbc<10>(JW); c.jw2 = rbc<11>(JW); }
+          T dk[NX];
+          tan_stage<T, DJ>(c, dS, K, dk);
+          // RK4 tangent update (mpcb_model.h rk4_tan: same operations)
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          if (st == 0) { dN[i] = dk[i]; dS[i] = fma(h2, dk[i], ev[i]); }
-          else if (st == 1) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h2, dk[i], ev[i]); }
-          else if (st == 2) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h, dk[i], ev[i]); }
-          else dN[i] = fma(h6, dN[i] + dk[i], ev[i]);
+          for (int i = 0; i < NX; ++i) {
+            if (st == 0) { dN[i] = dk[i]; dS[i] = fma(h2, dk[i], ev[i]); }
+            else if (st == 1) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h2, dk[i], ev[i]); }
+            else if (st == 2) { dN[i] = fma(T(2), dk[i], dN[i]); dS[i] = fma(h, dk[i], ev[i]); }
+            else dN[i] = fma(h6, dN[i] + dk[i], ev[i]);
+          }
+        } else {
+          // captured scalars of this RK stage (f_nom_lin order), each from a lane that holds it
+          T* const cs = cc0 + k * cc_k + st * LIN_N * SS;
+          if (t >= 3 && t < 6) {
+            cs[(2 * (t - 3)) * SS] = S;          // sf, st, sp
+            cs[(2 * (t - 3) + 1) * SS] = C;      // cf, ct, cp
+          }
+          if (t == 4) {
+            cs[6 * SS] = R;                      // ict
+            cs[7 * SS] = Tn;                     // tt
+          }
+          if (t >= 9 && t < 12) {
+            cs[(t + 5) * SS] = JW;               // jw0..2
+            cs[(t + 8) * SS] = Y;                // wx, wy, wz
+          }
+          if (t == 0) {
+            cs[8 * SS] = c.a;
+            cs[9 * SS] = c.cfst;
+            cs[10 * SS] = s;
+            cs[11 * SS] = c.r0;
+            cs[12 * SS] = c.r1;
+            cs[13 * SS] = c.r2;
+          }
         }
-      } else {
-        // captured scalars of this RK stage (f_nom_lin order), each from a lane that holds it
-        T* const cs = cc0 + k * cc_k + st * LIN_N * SS;
-        if (t >= 3 && t < 6) {
-          cs[(2 * (t - 3)) * SS] = S;          // sf, st, sp
-          cs[(2 * (t - 3) + 1) * SS] = C;      // cf, ct, cp
-        }
-        if (t == 4) {
-          cs[6 * SS] = R;                      // ict
-          cs[7 * SS] = Tn;                     // tt
-        }
-        if (t >= 9 && t < 12) {
-          cs[(t + 5) * SS] = JW;               // jw0..2
-          cs[(t + 8) * SS] = Y;                // wx, wy, wz
-        }
-        if (t == 0) {
-          cs[8 * SS] = c.a;
-          cs[9 * SS] = c.cfst;
-          cs[10 * SS] = s;
-          cs[11 * SS] = c.r0;
-          cs[12 * SS] = c.r1;
-          cs[13 * SS] = c.r2;
-        }
+        // RK4 stage update (lane-local; f = 0 on the input lanes)
+        if (st == 0) { XN = F; Y = fma(h2, F, X); }
+        else if (st == 1) { XN = fma(T(2), F, XN); Y = fma(h2, F, X); }
+        else if (st == 2) { XN = fma(T(2), F, XN); Y = fma(h, F, X); }
+        else Xn = fma(h6, XN + F, X);
       }
-      // RK4 stage update (lane-local; f = 0 on the input lanes)
-      if (st == 0) { XN = F; Y = fma(h2, F, X); }
-      else if (st == 1) { XN = fma(T(2), F, XN); Y = fma(h2, F, X); }
-      else if (st == 2) { XN = fma(T(2), F, XN); Y = fma(h, F, X); }
-      else Xn = fma(h6, XN + F, X);
-    }
+      if constexpr (!SLOW) {
+        // keep the fast pass's results ahead of the redo branch: left alone, the compiler sinks
+        // the tangent (used only when no redo follows) below it, out of the nominal chain's block
+        if constexpr (TAN) {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) asm volatile("" ::"v"(dN[i]));
+        }
+        asm volatile("" ::"v"(Xn));
+      }
+      return bad;
+    };
+    if (__any(interval(std::false_type{}))) (void)interval(std::true_type{});
     if constexpr (TAN) {
       // column var_col(tv) of [A_k | B_k] into the ABT2 rows: entry (i, tv) at i * ABT2_W + tv.
       // (Staging the wave's four records in LDS and writing them as 16-B vectors measured the

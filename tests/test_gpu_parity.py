@@ -574,6 +574,50 @@ def test_row_rollout_general_inertia_matches_oracle(dtype, mode):
     assert e_u.max() < tol and e_x.max() < tol and e_U.max() < tol
 
 
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_row_rollout_sincos_redo_matches_oracle(dtype):
+    """The row rollout's speculative interval (mpcb_rollout.hip `interval`): sin/cos without
+    range fallbacks, stages 1..3 (fp64) by angle addition over the stage offset, and a redo of the
+    interval with the full reduction when an angle lane leaves those ranges.  Waves mixing normal
+    instances with fast body rates (stage offsets above 1/8 rad) and huge roll angles (the
+    sin/cos large-argument fallback) against the oracle."""
+    N, B = 20, 40
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    x0 = inp['x0'].copy()
+    if dtype == 'f64':   # fast rates: offsets h/2 * rate > 1/8 (fp32 has no angle addition)
+        x0[0:12:2, 9:12] = [[14.0, -11.0, 9.0]]
+    big = np.zeros(B, bool)
+    big[1:12:4] = True
+    x0[big, 3] += 1.0e6 if dtype == 'f64' else 1.0e4   # beyond the reduction's range
+    m = _mpc(N, dtype, max_batch=B, path='split')
+    m.solve(x0, inp['xref'], inp['uref'])
+    torch.cuda.synchronize()
+    u0, X, U = (t.cpu().numpy().copy() for t in (m.get_control(), m.get_state_trajectory(),
+                                                  m.get_input_trajectory()))
+    assert (m.get_status().cpu().numpy() == 0).all() and np.isfinite(X).all()
+    if dtype == 'f64':
+        o = mpc_solve(x0, inp['xref'], inp['uref'], OcpSpec(N=N))
+        e_u, e_x, e_U = relerr(u0, o['u0']), relerr(X, o['X']), relerr(U, o['U'])
+        print(f'sincos redo f64: max rel err u0 {e_u.max():.2e} X {e_x.max():.2e} U {e_U.max():.2e}')
+        assert e_u.max() < 1e-9 and e_x.max() < 1e-9 and e_U.max() < 1e-9
+    else:
+        # a roll of 1e4 rad carries ~1e-3 rad of fp32 rounding, so those instances have no fp32
+        # oracle; the others are checked against it, and must come out bit for bit as in a batch
+        # without the large angles (the redo runs sc() = sc_core() on their lanes)
+        cast = lambda a: a.astype(np.float32).astype(np.float64)
+        o = mpc_solve(cast(x0[~big]), cast(inp['xref'][~big]), cast(inp['uref'][~big]), OcpSpec(N=N))
+        e_u = relerr(u0[~big], o['u0'])
+        e_U = relerr(U[~big], o['U'])
+        print(f'sincos redo f32: max rel err u0 {e_u.max():.2e} U {e_U.max():.2e}')
+        assert e_u.max() < 5e-5 and e_U.max() < 5e-5
+        x1 = x0.copy()
+        x1[big, 3] -= 1.0e4
+        m.solve(x1, inp['xref'], inp['uref'])
+        torch.cuda.synchronize()
+        assert np.array_equal(m.get_control().cpu().numpy()[~big], u0[~big])
+        assert np.array_equal(m.get_state_trajectory().cpu().numpy()[~big], X[~big])
+
+
 @pytest.mark.parametrize('N', [20, 7])
 def test_rollout_tangent_export_equals_captured_scalar_path(N):
     """fp64 small chunks: the rollout that integrates the sensitivities and exports [A|B]
