@@ -171,8 +171,10 @@ template <bool W32> struct Masks {
   __device__ static __forceinline__ int clz(M v) { if constexpr (W32) return __builtin_clz(v); else return __clzll(v); }
 };
 
+WT_TABLE(g_wt_p3)
 template <class T, bool BOX, bool W32 = false, bool ITER = false>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
+  if constexpr (!BOX) WT(g_wt_p3, 0);
   using Mk = Masks<W32>;
   using M = typename Mk::M;
   constexpr int WB = Mk::WB;
@@ -639,11 +641,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       rload(k + FD < N ? k + FD : N - 1, slot_tag);
       ASTAMP(6);
     };
+    if constexpr (!BOX) WT(g_wt_p3, 1);
     for (int k0 = 0; k0 < N; k0 += FD) {
       static_for<FD>([&](auto s) {
         if (k0 + decltype(s)::value < N) stage(k0 + decltype(s)::value, s);
       });
     }
+    if constexpr (!BOX) WT(g_wt_p3, 2);
     // outputs of this pass: staged rows leave as 16-B vectors once the pass is known to be final
     // (the unconstrained pass; the active-set pass that converged or used the last iteration)
     if (stage_out && stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
@@ -736,6 +740,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
 #endif
   if constexpr (!BOX) finish();   // (the box kernel finishes each instance as it converges)
+  if constexpr (!BOX) WT(g_wt_p3, 3);
 }
 
 }  // namespace asq
@@ -802,6 +807,9 @@ template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 }  // namespace mpcb
 
 #ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_wt_p3(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+}
 extern "C" int mpcb_debug_stamps_as(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_astamps), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -2;
 }

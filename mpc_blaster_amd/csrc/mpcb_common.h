@@ -32,6 +32,21 @@ template <int BOX> struct Rec { static constexpr int n = BOX ? 24 : 4; };
 // operation at each exchange.  Valid only for 64-thread (one-wave) workgroups.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
 
+// Diagnostic builds only (-DMPCB_STAMPS): per-wave timeline of a kernel in its translation unit's
+// table, s_memrealtime (100 MHz, one clock for the whole chip) at slot 0 entry, 1 loop start,
+// 2 loop end, 3 exit; lane 0 of each of the first 4096 workgroups writes it (a vector store).
+#ifdef MPCB_STAMPS
+#define WT_TABLE(name) __device__ unsigned long long name[4096 * 4];
+#define WT(name, slot)                                                              \
+  {                                                                                 \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) name[blockIdx.x * 4 + (slot)] = t_; \
+  }
+#else
+#define WT_TABLE(name)
+#define WT(name, slot)
+#endif
+
 // f(std::integral_constant<int, i>{}) for i = 0 .. n-1 (compile-time lane indices for DPP)
 template <int n, class F, int i = 0> __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (i < n) {

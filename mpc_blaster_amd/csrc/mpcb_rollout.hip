@@ -125,8 +125,10 @@ __device__ __forceinline__ void tan_stage(const StageSc<T>& c, const T* __restri
 // ABT2 rows (mpcb_kernels.h) that P2 then reads instead of integrating them (SplitArgs::tin).  The
 // tangent of stage s is independent of the nominal stage s + 1, so the two chains interleave in
 // one basic block; no captured-scalar record (CC) is written.
+WT_TABLE(g_wt_p1)
 template <class T, bool ITER, bool DJ, bool TAN>
 __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
+  WT(g_wt_p1, 0);
   const int lane = threadIdx.x;
   const int t = lane & 15;                 // row lane
   const int q = lane >> 4;                 // instance within the wavefront's quad
@@ -225,28 +227,43 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char row_dyn[];
   T* const lu = reinterpret_cast<T*>(row_dyn);          // [GROUPS][N][NU]: u of the stage
   T* const lx = lu + GROUPS * N * NU;                    // ITER: [GROUPS][N + 1][NX]: xbar
+  // X: x_t (t < 12) / u_{t-12} (t >= 12) of the interval's start; x0's load is issued first
+  T X = T(0);
+  if (!ITER && t < NX) X = a.x0[b * a.x0_sb + t];
   {
-    const int nu_e = N * NU, nx_e = (N + 1) * NX;
-    for (int e = lane; e < GROUPS * nu_e; e += 64) {
-      const int g = e / nu_e, r = e - g * nu_e;
-      const int64_t cg = qd * SS + g < nb ? qd * SS + g : nb - 1;
-      lu[e] = ITER ? a.ubar[(a.b0 + cg) * (int64_t)nu_e + r] : a.uref[(a.b0 + cg) * a.uref_sb + r];
-    }
-    if (ITER) {
-      for (int e = lane; e < GROUPS * nx_e; e += 64) {
-        const int g = e / nx_e, r = e - g * nx_e;
-        const int64_t cg = qd * SS + g < nb ? qd * SS + g : nb - 1;
-        lx[e] = a.xbar[(a.b0 + cg) * (int64_t)nx_e + r];
+    // eight loads in flight per lane before their LDS writes (one at a time, the staging was a
+    // chain of global-load round trips: 2.5 us of the c2 wave's prologue), the group by compares
+    auto stage_in = [&](T* dst, const int per, auto&& src) {
+      const int total = GROUPS * per;
+      for (int e0 = lane; e0 < total; e0 += 64 * 8) {
+        T v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + 64 * u;
+          const int g = (e >= per) + (e >= 2 * per) + (e >= 3 * per);
+          const int64_t cg = qd * SS + g < nb ? qd * SS + g : nb - 1;
+          v[u] = e < total ? src(a.b0 + cg, e - g * per) : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + 64 * u < total) dst[e0 + 64 * u] = v[u];
       }
+    };
+    static_assert(GROUPS == 4, "stage_in's group compares");
+    const int nu_e = N * NU, nx_e = (N + 1) * NX;
+    if constexpr (ITER) {
+      stage_in(lu, nu_e, [&](int64_t bb, int r) { return a.ubar[bb * (int64_t)nu_e + r]; });
+      stage_in(lx, nx_e, [&](int64_t bb, int r) { return a.xbar[bb * (int64_t)nx_e + r]; });
+    } else {
+      stage_in(lu, nu_e, [&](int64_t bb, int r) { return a.uref[bb * a.uref_sb + r]; });
     }
     wave_lds_sync();
   }
   const T* const lxq = lx + q * (N + 1) * NX;
   const T* const luq = lu + q * N * NU;
-  // X: x_t (t < 12) / u_{t-12} (t >= 12) of the interval's start
-  T X = T(0);
-  if (t < NX) X = ITER ? lxq[t] : a.x0[b * a.x0_sb + t];
+  if (ITER && t < NX) X = lxq[t];
 
+  WT(g_wt_p1, 1);
   for (int k = 0; k < N; ++k) {
     if (ITER && t < NX && k) X = lxq[k * NX + t];
     if (t >= NX) X = luq[k * NU + (t - NX)];
@@ -413,12 +430,14 @@ __global__ void __launch_bounds__(64) nominal_row_kernel(SplitArgs<T> a) {
       X = Xn;
     }
   }
+  WT(g_wt_p1, 2);
   if (t < NX) {
     if (ITER) X = lxq[N * NX + t];
   } else {
     X = T(0);
   }
   xu0[N * xu_k + t * SS] = X;
+  WT(g_wt_p1, 3);
 }
 
 // dynamic LDS of the row rollout: the wave's staged u (and, iterate mode, xbar) records
@@ -452,6 +471,11 @@ template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStrea
 }
 
 template hipError_t launch_nominal_row<double>(const SplitArgs<double>&, hipStream_t);
+#ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_wt_p1(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+}
+#endif
 template hipError_t launch_nominal_row<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb

@@ -463,8 +463,10 @@ template <int L> __device__ __forceinline__ double rbc64(double v) {
   return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
 }
 
+WT_TABLE(g_wt_p2)
 template <class T, bool EXPORT, bool ITER = false, bool TIN = false>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
+  WT(g_wt_p2, 0);
   // fp64 DPP path: every exchange of the stage by row broadcasts -- Y reads P straight out of
   // the lanes' unsymmetrised columns (lane max(i, l) owns entry (i, l): mpcb_dpp_gen.h ypn_bc),
   // the stage-cost term S v, H_uu and h_u by broadcasts -- so P needs no LDS transpose and the
@@ -591,6 +593,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   int buf = 0;
   wave_lds_sync();
   STAMP_INIT();
+  WT(g_wt_p2, 1);
   for (int k = N - 1; k >= 0; --k) {
     T col[NX];
     T ptr = T(0);   // R32: this lane's entry of p + P gap
@@ -881,6 +884,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     STAMP(9);
   }
   STAMP_DONE();
+  WT(g_wt_p2, 2);
   if (valid && j == NX) a.status[b] = qp_ok ? MPCB_STATUS_OK : MPCB_STATUS_QP_FAIL;
   if (valid && !a.fwd && j >= NX) {
     // rollout mode without trajectories: dx_0 = 0 so u0 = ubar_0 + kff_0
@@ -889,6 +893,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     const bool fin = isfin(u);
     if (!fin) a.status[b] = MPCB_STATUS_NAN;
   }
+  WT(g_wt_p2, 3);
 }
 
 // P3 LDS carve (dynamic): two stage images (XU | KR | CC) for the one-stage-ahead DMA, plus the
@@ -1175,6 +1180,11 @@ template int64_t split_elems_per_instance<float>(int, int, int);
 
 #ifdef MPCB_STAMPS
 // (same translation unit as g_stamps: the library is built without -fgpu-rdc)
+#ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_wt_p2(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+}
+#endif
 extern "C" int mpcb_debug_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
 }
