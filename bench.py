@@ -238,7 +238,9 @@ def run(w, world, rank, dev, steps, warmup, stub=None, dump_gather=None):
             t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=odev)
             dist.all_reduce(t)
             qp['fwd_passes'], qp['bwd_stages'] = float(t[0]) / world, float(t[1]) / world
-    path = 'split (3 kernels)' if mpc.path == 'split' else 'fused (1 kernel)'
+    two = w['batch'] <= 16384 and w['dtype'] == 'f64'   # P1 + P2 in one launch (row_riccati_kernel)
+    path = (('split (2 kernels: rollout+Riccati, forward)' if two else 'split (3 kernels)')
+            if mpc.path == 'split' else 'fused (1 kernel)')
     mpc.close()
     return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path, phase_ms=phase_ms,
                 split=path.startswith('split'), qp=qp)
@@ -251,8 +253,9 @@ def phase_kernels(w):
       nominal  4 f evaluations (4 x 300) of the RK4 rollout; with the tangent export (fp64 chunks
                <= 16384: c2) the RK4 rollout and its sensitivities, 21,996;
       riccati  RK4 sensitivities minus those f evaluations plus the Riccati backward
-               (21,996 - 1,200 + 12,309 = 33,105); with the tangent export the Riccati backward
-               alone, 12,309;
+               (21,996 - 1,200 + 12,309 = 33,105); with the tangent export (c2) P1 and P2 are ONE
+               launch per quad (row_riccati_kernel), the rollout with sensitivities plus the
+               Riccati backward, 21,996 + 12,309 = 34,305, and the "nominal" phase is empty;
       forward  du = K dx + k, dx' = [A|B] (dx, du) (+ gap): 480;
       box      the active-set kernel (c4): per masked backward stage recomputed 12,309 (the Riccati
                algebra over the cached [A|B]), per forward stage 480 + the multipliers
@@ -262,6 +265,8 @@ def phase_kernels(w):
     t = 'float' if w['dtype'] == 'f32' else 'double'
     small = w['batch'] <= 16384
     tin = small and w['dtype'] == 'f64'
+    if tin:   # P1 and P2 in one kernel per quad (mpcb_split.hip row_riccati_kernel, MPCB_FUSE_P12)
+        return {'riccati': 'row_riccati_kernel<false, true>', 'forward': f'fwd_rm_kernel<{t}, false>'}
     # (the rollout-mode instantiations: the mode is a template argument of P1, P2 and P3; the row
     # rollout's <T, ITER, DJ, TAN>: DJ = the reference's diagonal inertia)
     names = {'nominal': f'nominal_row_kernel<{t}, false, true, {"true" if tin else "false"}>' if small
@@ -281,8 +286,9 @@ def kernel_flops(w, r, phase):
     tin = B <= 16384 and w['dtype'] == 'f64'
     if phase == 'nominal':
         return (FLOP_PER_INTERVAL_ROLLOUT_TAN if tin else 1200) * N * B
-    if phase == 'riccati':
-        return (FLOP_PER_INTERVAL_RICCATI_TIN if tin else FLOP_PER_INTERVAL_RICCATI) * N * B
+    if phase == 'riccati':   # (tin: the fused rollout + Riccati kernel)
+        return ((FLOP_PER_INTERVAL_ROLLOUT_TAN + FLOP_PER_INTERVAL_RICCATI_TIN) if tin
+                else FLOP_PER_INTERVAL_RICCATI) * N * B
     if w['box']:
         q = r['qp']
         return 12309 * q['bwd_stages'] + (480 + 136) * N * q['fwd_passes']

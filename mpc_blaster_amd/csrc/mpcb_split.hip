@@ -65,6 +65,12 @@
 #endif
 
 namespace mpcb {
+WT_TABLE(g_wt_p1)
+}  // namespace mpcb
+
+#include "mpcb_row.h"
+
+namespace mpcb {
 
 #ifdef MPCB_STAMPS
 // Diagnostic build only: per-region cycle counts of the Riccati stage loop of workgroup 0
@@ -1095,6 +1101,22 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs
   riccati_body<double, EXPORT, ITER, TIN>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
+// c2 (fp64 small chunks with the tangent export): P1 and P2 of a quad in ONE kernel.  Nothing
+// crosses quads between them, so the wave that rolled its four instances out runs their Riccati
+// recursion straight after, without the kernel boundary (its drain and cache write-back) and the
+// second kernel's launch and prologue; its own ABT2 / XU stores are ordered before its loads by
+// the workgroup fence (MPCB_FUSE_P12=0: two kernels).
+#ifndef MPCB_FUSE_P12
+#define MPCB_FUSE_P12 1
+#endif
+template <bool ITER, bool DJ>
+__global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_kernel(SplitArgs<double> a) {
+  row_body<double, ITER, DJ, true>(a);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+}
+
 template <class T, bool USE_CC, bool ITER>
 static hipError_t launch_forward_m(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
   constexpr size_t bytes = FwdLds<T, USE_CC>::BYTES;
@@ -1116,7 +1138,23 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (a.quad_p1 == 2) {
+  const bool fuse = sizeof(T) == 8 && MPCB_FUSE_P12 && a.quad_p1 == 2 && a.tin && !a.small;
+  if (fuse) {
+    // (the phase events: "nominal" empty, "riccati" the fused kernel)
+    if (ev) (void)hipEventRecord(ev[1], st);
+    const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
+    const size_t lds = row_lds_bytes(a);
+    const bool it = a.mode == MPCB_MODE_ITERATE;   // (the row body's mode is always a template argument)
+    if constexpr (sizeof(T) == 8) {
+      if (row_dj(a)) {
+        if (it) hipLaunchKernelGGL((row_riccati_kernel<true, true>), grid, dim3(64), lds, st, a);
+        else hipLaunchKernelGGL((row_riccati_kernel<false, true>), grid, dim3(64), lds, st, a);
+      } else {
+        if (it) hipLaunchKernelGGL((row_riccati_kernel<true, false>), grid, dim3(64), lds, st, a);
+        else hipLaunchKernelGGL((row_riccati_kernel<false, false>), grid, dim3(64), lds, st, a);
+      }
+    }
+  } else if (a.quad_p1 == 2) {
     const hipError_t e = launch_nominal_row<T>(a, st);
     if (e != hipSuccess) return e;
   } else if (a.quad_p1) {
@@ -1128,7 +1166,7 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     hipLaunchKernelGGL((nominal_kernel<T, true>), dim3(gw), dim3(WAVE), 0, st, a);
   else
     hipLaunchKernelGGL((nominal_kernel<T, false>), dim3(gw), dim3(WAVE), 0, st, a);
-  if (ev) (void)hipEventRecord(ev[1], st);
+  if (ev && !fuse) (void)hipEventRecord(ev[1], st);
   if (a.small) {   // linearisation + Riccati + forward over the cached [A|B] (mpcb_box.hip)
     hipError_t e = launch_small<T>(a, st);
     if (ev) (void)hipEventRecord(ev[2], st);
@@ -1147,7 +1185,9 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   } else {
     // one fp64 instantiation per mode (export guarded at run time): measured leaner than the
     // export-free one, which LLVM schedules into 368 bytes of scratch spill
-    if (a.tin) {
+    if (fuse) {
+      // (P2 ran in row_riccati_kernel)
+    } else if (a.tin) {
       if (it) hipLaunchKernelGGL((riccati_kernel_f64<true, true, true>), dim3(g64), dim3(64), 0, st, a);
       else hipLaunchKernelGGL((riccati_kernel_f64<true, false, true>), dim3(g64), dim3(64), 0, st, a);
     } else if (it) {
