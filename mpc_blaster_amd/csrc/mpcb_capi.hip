@@ -263,6 +263,9 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     // [A|B] instead of integrating it
     h->tin = (h->quad_p1 == 2 && !h->small && f64) ? 1 : 0;
     if (const char* e = getenv("MPCB_P1_TAN")) if (atoi(e) == 0) h->tin = 0;
+    // ... and P2 runs in the same launch (row_riccati_kernel) unless MPCB_FUSE_P12=0
+    if (h->tin)
+      if (const char* e = getenv("MPCB_FUSE_P12")) if (atoi(e) == 0) h->tin = 2;
     const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
     const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
                             : split_elems_per_instance<float>(cfg->N, 1, ab);

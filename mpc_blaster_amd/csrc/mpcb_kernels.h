@@ -130,7 +130,9 @@ struct SplitArgs {
                      // mpcb_rollout.hip), 1 = a lane quad per instance (sin/cos split), 0 = a
                      // thread per instance
   int tin;           // 1: the row rollout integrated the tangents and exported [A|B] as the ABT2
-                     // rows (mpcb_rollout.hip TAN); P2 reads its columns from them (no CC record)
+                     // rows (mpcb_row.h TAN); P2 reads its columns from them (no CC record), in
+                     // the same launch (row_riccati_kernel); 2: the same as two launches
+                     // (MPCB_FUSE_P12=0)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
   int rm;            // 1: P2 writes the row-major exports (AB2, ABT2, GH2, KR2 in a.AB/a.ABT/a.GH/a.KR)
   int imajor;        // row-major exports instance-major (an instance's N records contiguous: the

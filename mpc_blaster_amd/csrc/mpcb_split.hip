@@ -1105,7 +1105,7 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs
 // crosses quads between them, so the wave that rolled its four instances out runs their Riccati
 // recursion straight after, without the kernel boundary (its drain and cache write-back) and the
 // second kernel's launch and prologue; its own ABT2 / XU stores are ordered before its loads by
-// the workgroup fence (MPCB_FUSE_P12=0: two kernels).
+// the workgroup fence (MPCB_FUSE_P12=0 at build or run time: two kernels).
 #ifndef MPCB_FUSE_P12
 #define MPCB_FUSE_P12 1
 #endif
@@ -1138,7 +1138,7 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned gw = (unsigned)((a.nb + WAVE - 1) / WAVE);
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
-  const bool fuse = sizeof(T) == 8 && MPCB_FUSE_P12 && a.quad_p1 == 2 && a.tin && !a.small;
+  const bool fuse = sizeof(T) == 8 && MPCB_FUSE_P12 && a.quad_p1 == 2 && a.tin == 1 && !a.small;
   if (fuse) {
     // (the phase events: "nominal" empty, "riccati" the fused kernel)
     if (ev) (void)hipEventRecord(ev[1], st);
@@ -1221,6 +1221,9 @@ template int64_t split_elems_per_instance<float>(int, int, int);
 #ifdef MPCB_STAMPS
 // (same translation unit as g_stamps: the library is built without -fgpu-rdc)
 #ifdef MPCB_STAMPS
+extern "C" int mpcb_debug_wt_p1f(unsigned long long* out) {   // the row body inside row_riccati_kernel
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+}
 extern "C" int mpcb_debug_wt_p2(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
 }

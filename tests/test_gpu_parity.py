@@ -618,6 +618,33 @@ def test_row_rollout_sincos_redo_matches_oracle(dtype):
         assert np.array_equal(m.get_state_trajectory().cpu().numpy()[~big], X[~big])
 
 
+@pytest.mark.parametrize('mode', ['rollout', 'iterate'])
+def test_fused_rollout_riccati_equals_two_kernels(mode):
+    """c2's row_riccati_kernel (P1 and P2 of a quad in one launch) against the same two bodies as
+    two launches (MPCB_FUSE_P12=0): the same operations, so the same bits."""
+    N, B = 20, 45
+    inp = make_inputs('c2', ids=np.arange(B, dtype=np.uint64), N=N)
+    rng = np.random.default_rng(21)
+    xbar = inp['xref'] + rng.normal(scale=0.05, size=(B, N + 1, 12))
+    ubar = inp['uref'] + rng.normal(scale=1.0, size=(B, N, 4))
+    res = []
+    for fuse in ('1', '0'):
+        os.environ['MPCB_FUSE_P12'] = fuse
+        try:
+            m = _mpc(N, 'f64', max_batch=B, path='split')
+            if mode == 'iterate':
+                m.solve_iterate(inp['x0'], xbar, ubar, inp['xref'], inp['uref'])
+            else:
+                m.solve(inp['x0'], inp['xref'], inp['uref'])
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop('MPCB_FUSE_P12')
+        res.append([t.cpu().numpy().copy() for t in (m.get_control(), m.get_state_trajectory(),
+                                                      m.get_input_trajectory(), m.get_status())])
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize('N', [20, 7])
 def test_rollout_tangent_export_equals_captured_scalar_path(N):
     """fp64 small chunks: the rollout that integrates the sensitivities and exports [A|B]

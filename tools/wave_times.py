@@ -27,9 +27,11 @@ torch.cuda.synchronize()
 lib = _lib.load()
 waves = B // 4
 starts = {}
-for name in ('p1', 'p2', 'p3'):
+# (c2 runs P1 inside row_riccati_kernel: its table is p1f; MPCB_FUSE_P12=0 builds: p1)
+for name in ('p1f' if os.environ.get('WT_P1', 'p1f') == 'p1f' else 'p1', 'p2', 'p3'):
     buf = (ctypes.c_ulonglong * (4096 * 4))()
     f = getattr(lib, f'mpcb_debug_wt_{name}')
+    name = name[:2]
     f.argtypes = [ctypes.c_void_p]
     assert f(buf) == 0
     t = np.array(buf, dtype=np.float64).reshape(4096, 4)[:waves] * 0.01   # us
