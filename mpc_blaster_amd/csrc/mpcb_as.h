@@ -1,0 +1,738 @@
+// mpcb_as.h -- the body of the active-set kernel and of the unconstrained 16-lane forward pass
+// (as_body), shared by mpcb_as.hip (their kernels) and mpcb_split.hip (c2's fused kernel).  The
+// design notes are at the top of mpcb_as.hip.  Stamp tables live in the owning translation unit
+// (MPCB_AS_OWNER, mpcb_as.hip) only: without -fgpu-rdc a device variable cannot be shared.
+#pragma once
+
+#if defined(MPCB_STAMPS) && defined(MPCB_AS_OWNER)
+#define MPCB_AS_STAMPS 1
+#define AS_WT(slot) WT(g_wt_p3, slot)
+#else
+#define AS_WT(slot)
+#endif
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "../../include/mpcb.h"
+#include "mpcb_kernels.h"
+#include "mpcb_common.h"
+#include "mpcb_split.h"
+
+#ifndef MPCB_AS_WAVES
+#define MPCB_AS_WAVES 2
+#endif
+#ifndef MPCB_AS_FDEPTH   // forward-pass prefetch ring (stages): active-set kernel
+#define MPCB_AS_FDEPTH 2
+#endif
+#ifndef MPCB_AS_ITER_T   // the mode as a template argument (as in P1 / P2 / P3)
+#define MPCB_AS_ITER_T 1
+#endif
+#ifndef MPCB_FWD_FDEPTH  // the same for the unconstrained forward pass (fwd_rm_kernel)
+#define MPCB_FWD_FDEPTH 2
+#endif
+
+namespace mpcb {
+namespace asq {
+
+#ifdef MPCB_AS_STAMPS
+// Diagnostic build only: per-region s_memtime cycles of workgroup 0, wave-summed over the whole
+// kernel ([0] backward init, [1..3] backward stage parts, [4..6] forward stage parts, [7] forward
+// tail + active-set update, [8] iterations, [9] backward stages), read by mpcb_debug_stamps_as()
+__device__ unsigned long long g_astamps[12];
+#define ASTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ast_acc[i] += t_ - ast_prev; ast_prev = t_; }
+#else
+#define ASTAMP(i)
+#endif
+
+// ---- DPP row broadcasts (16-lane rows = one instance) ---------------------------------------
+// Inline asm: the compiler's hazard recognizer does not look inside, so every block starts with
+// s_nop 4 (VALU / EXEC write -> DPP read wait states); no source is written inside a block.
+// Every block runs with all 16 lanes of each row active (group-uniform control flow only).
+#define ASQ_I(op, d, s, b, l) op " %" #d ", %" #s ", %" #b " row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+#define ASQ_A(op, d, s, b, l) op " %" #d ", |%" #s "|, |%" #b "| row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+// acc[l & 3] += bcast_l(%4) * %(5 + l)
+#define ASQ_DOT12(M, op)                                                                           \
+  M(op, 0, 4, 5, 0) M(op, 1, 4, 6, 1) M(op, 2, 4, 7, 2) M(op, 3, 4, 8, 3) M(op, 0, 4, 9, 4)       \
+  M(op, 1, 4, 10, 5) M(op, 2, 4, 11, 6) M(op, 3, 4, 12, 7) M(op, 0, 4, 13, 8) M(op, 1, 4, 14, 9)   \
+  M(op, 2, 4, 15, 10) M(op, 3, 4, 16, 11)
+#define ASQ_DOT16(M, op) ASQ_DOT12(M, op) M(op, 0, 4, 17, 12) M(op, 1, 4, 18, 13) M(op, 2, 4, 19, 14) M(op, 3, 4, 20, 15)
+#define ASQ_OUT4(acc) "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+#define ASQ_IN12(z, r) "v"(z), "v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), \
+                       "v"(r[7]), "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11])
+#define ASQ_IN16(z, r) ASQ_IN12(z, r), "v"(r[12]), "v"(r[13]), "v"(r[14]), "v"(r[15])
+
+// fp32: acc[0] += sum_{l = 0 mod 4} ..., acc[1..3] = (their sums from zero): the first product of
+// accumulators 1..3 is a v_mul_f32_dpp instead of a v_fmac into a zeroed register (the zeroing
+// moves were ~5 % of a forward stage's instructions).  fp64 has no DPP form of v_mul_f64 (VOP3).
+#define ASQ_FIRST(M, mop) M(mop, 1, 4, 6, 1) M(mop, 2, 4, 7, 2) M(mop, 3, 4, 8, 3)
+#define ASQ_DOT12Z(M, op, mop)                                                                      \
+  M(op, 0, 4, 5, 0) ASQ_FIRST(M, mop) M(op, 0, 4, 9, 4) M(op, 1, 4, 10, 5) M(op, 2, 4, 11, 6)     \
+  M(op, 3, 4, 12, 7) M(op, 0, 4, 13, 8) M(op, 1, 4, 14, 9) M(op, 2, 4, 15, 10) M(op, 3, 4, 16, 11)
+#define ASQ_DOT16Z(M, op, mop) ASQ_DOT12Z(M, op, mop) M(op, 0, 4, 17, 12) M(op, 1, 4, 18, 13) M(op, 2, 4, 19, 14) M(op, 3, 4, 20, 15)
+#define ASQ_OUT4Z(acc) "+v"(acc[0]), "=&v"(acc[1]), "=&v"(acc[2]), "=&v"(acc[3])
+
+// acc[*] += sum_{l<12} bcast_l(z) * r[l]   (fp32: acc[1..3] need not be initialised)
+__device__ __forceinline__ void dot12(float (&acc)[4], float z, const float (&r)[12]) {
+  asm("s_nop 4\n\t" ASQ_DOT12Z(ASQ_I, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN12(z, r));
+}
+__device__ __forceinline__ void dot12(double (&acc)[4], double z, const double (&r)[12]) {
+  asm("s_nop 4\n\t" ASQ_DOT12(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
+}
+// acc[*] += sum_{l<16} bcast_l(z) * r[l]   (fp32: acc[1..3] need not be initialised)
+__device__ __forceinline__ void dot16(float (&acc)[4], float z, const float (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16Z(ASQ_I, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN16(z, r));
+}
+__device__ __forceinline__ void dot16(double (&acc)[4], double z, const double (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_I, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+// acc[*] += sum_{l<16} |bcast_l(z) * r[l]|   (fp32: acc[1..3] need not be initialised)
+__device__ __forceinline__ void dot16abs(float (&acc)[4], float z, const float (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16Z(ASQ_A, "v_fmac_f32_dpp", "v_mul_f32_dpp") : ASQ_OUT4Z(acc) : ASQ_IN16(z, r));
+}
+__device__ __forceinline__ void dot16abs(double (&acc)[4], double z, const double (&r)[16]) {
+  asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
+}
+// acc[i] += bcast_i(a) * b, i < 12 (lane i's a feeds accumulator i); the fp64 form is
+// mpcb_split.h fmac12_diag
+#define ASQ_D(d, l) "v_fmac_f32_dpp %" #d ", %12, %13 row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void diag12(float (&acc)[12], float a, float b) {
+  asm("s_nop 4\n\t" ASQ_D(0, 0) ASQ_D(1, 1) ASQ_D(2, 2) ASQ_D(3, 3) ASQ_D(4, 4) ASQ_D(5, 5) ASQ_D(6, 6)
+      ASQ_D(7, 7) ASQ_D(8, 8) ASQ_D(9, 9) ASQ_D(10, 10) ASQ_D(11, 11)
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+        "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11])
+      : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void diag12(double (&acc)[12], double a, double b) { fmac12_diag(acc, a, b); }
+#undef ASQ_D
+
+template <class T> __device__ __forceinline__ T sum4(const T (&a)[4]) { return (a[0] + a[1]) + (a[2] + a[3]); }
+
+// lane L's value in every lane of its row (v_mov_b32_dpp row_newbcast:L)
+template <int L> __device__ __forceinline__ unsigned bcu(unsigned v) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xF, 0xF, true);
+}
+template <int L> __device__ __forceinline__ int bc(int v) { return (int)bcu<L>((unsigned)v); }
+template <int L> __device__ __forceinline__ float bc(float v) { return __uint_as_float(bcu<L>(__float_as_uint(v))); }
+template <int L> __device__ __forceinline__ unsigned bc(unsigned v) { return bcu<L>(v); }
+template <int L> __device__ __forceinline__ uint64_t bc(uint64_t v) {
+  return ((uint64_t)bcu<L>((unsigned)(v >> 32)) << 32) | bcu<L>((unsigned)v);
+}
+template <int L> __device__ __forceinline__ double bc(double v) {
+  return __builtin_bit_cast(double, bc<L>(__builtin_bit_cast(uint64_t, v)));
+}
+
+// stage-invariant addressing of one quad-blocked workspace array (mpcb_split.h soa()):
+// element e of the stage-k record of this lane's instance = p0 + k * stride + e * SS
+template <class T> struct Arr {
+  T* p0;
+  int64_t stride;
+  __device__ __forceinline__ T* at(int k) const { return p0 + (int64_t)k * stride; }
+};
+// quad-blocked (soa) array: element e of the record at p0 + k * stride + e * SS
+template <class T> __device__ __forceinline__ Arr<T> arr(T* base, int rec, int64_t nq, int64_t c) {
+  return Arr<T>{base ? base + ((c >> 2) * rec) * SS + (c & (SS - 1)) : nullptr, nq * rec * SS};
+}
+// row-major export (rec2): element e of the record at p0 + k * stride + e
+template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int64_t nq, int64_t c, int N, int imaj) {
+  // (mpcb_split.h rec2: instance-major or stage-major)
+  if (imaj) return Arr<T>{base ? base + c * N * (int64_t)rec : nullptr, rec};
+  return Arr<T>{base ? base + ((c >> 2) * SS + (c & (SS - 1))) * rec : nullptr, nq * SS * rec};
+}
+
+// BOX: the active-set iterations; !BOX: one forward pass over P2's gains (unconstrained small
+// chunks, SplitArgs::fwd16)
+// Output staging: a pass's X / U rows go to LDS (one [(N+1)*12 | N*4] block per instance) and
+// leave as 16-B vector stores after the pass.  Stores issued inside the stage loop would sit in
+// the same in-order vmcnt queue as the prefetch loads, so every wait for a prefetched row also
+// waited for the write acknowledgements of the previous stages' scattered 4/8-B output stores.
+constexpr int OUT_NMAX = 64;   // longer horizons store directly
+template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
+
+// Stage masks (active sets, violations: bit k = stage k) of a horizon N <= 32 in 32-bit registers
+// (W32: half the VALU of every mask shift / or in the stage loops), else 64-bit.
+template <bool W32> struct Masks {
+  using M = std::conditional_t<W32, uint32_t, uint64_t>;
+  static constexpr int WB = W32 ? 32 : 64;
+  __device__ static __forceinline__ int popc(M v) { if constexpr (W32) return __builtin_popcount(v); else return __popcll(v); }
+  __device__ static __forceinline__ int ffs(M v) { if constexpr (W32) return __builtin_ffs((int)v); else return __ffsll((long long)v); }
+  __device__ static __forceinline__ int clz(M v) { if constexpr (W32) return __builtin_clz(v); else return __clzll(v); }
+};
+
+#ifdef MPCB_AS_STAMPS
+WT_TABLE(g_wt_p3)
+#endif
+template <class T, bool BOX, bool W32 = false, bool ITER = false>
+__device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
+  if constexpr (!BOX) AS_WT(0);
+  using Mk = Masks<W32>;
+  using M = typename Mk::M;
+  constexpr int WB = Mk::WB;
+  __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
+  extern __shared__ __attribute__((aligned(16))) unsigned char as_dyn[];
+  const int lane = threadIdx.x;
+  const int q = lane >> 4;
+  const int j = lane & 15;
+  const int jx = j < NX ? j : 0;
+  const int ju = j >= NX ? j - NX : 0;
+  const bool stl = j < NX;                          // state lane (else input lane ju)
+  const uint64_t mst = lane_mask(stl);
+  T* const PX = lds_px[q];
+  const int64_t nb = a.nb;
+  const int N = a.N;
+  // the RK4 tangent's position entry of a velocity column, h/6 * (1 + 2 + 2 + 1) as the tangent
+  // computes it: the same [A|B] column as P2's (mpcb_split.hip riccati_body hv), whose snapshots
+  // the first masked pass restarts from
+  const T h = (a.h / T(6)) * T(6);
+  const Weights<T>& W = *a.W;
+  const bool iterate = MPCB_AS_ITER_T ? ITER : a.mode == MPCB_MODE_ITERATE;   // (see riccati_body)
+  const T lbm = W.lbu[ju], ubm = W.ubu[ju];
+  constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
+  const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
+  const int64_t nq = (nb + SS - 1) / SS;
+  // The group's instance and its workspace records.  Box kernel with a work counter (a.as_queue):
+  // the grid holds the waves the machine keeps resident, and a group whose instance finished
+  // takes the next one from the counter, so a wave does not carry three idle groups while its
+  // slowest instance finishes (3.8 active-set passes per instance, 5.2 per wave with fixed quads).
+  bool valid;
+  int64_t c, b;
+  const T *xr, *ur, *xrN;
+  Arr<T> XU, GP, AB, ABT, GH, KR, PS;
+  auto bind = [&](int64_t c_raw) {
+    valid = c_raw < nb;
+    c = valid ? c_raw : nb - 1;       // an empty group shadows the last instance
+    b = a.b0 + c;
+    xr = a.xref + b * a.xref_sb;
+    ur = a.uref + b * a.uref_sb;
+    xrN = xr + (int64_t)N * NX;
+    XU = arr(a.XU, XU_REC, nq, c);
+    GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
+    AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c, N, a.imajor);
+    ABT = arr2(a.ABT, ABT2_REC, nq, c, N, a.imajor);
+    GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c, N, a.imajor);
+    KR = arr2(a.KR, KR2_REC, nq, c, N, a.imajor);
+    PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c, N, a.imajor);
+  };
+  bind((int64_t)blockIdx.x * GROUPS + q);
+  const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
+  // (Measured and dropped, round 4: stores from every lane with the masked-out ones into a
+  // per-lane scratch, so that the waits for the prefetched loads no longer drain the stores --
+  // 3.15 -> 4.73 ms, the scratch writes cost more than the drains; prefetching the backward
+  // stages for every group: no change.)
+  // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
+  const int cslot = j < 3 ? j : j - 3;
+  // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
+  // the stage cost of direction j, when a backward stage needs it
+  __shared__ T SW[NZ * NZ];
+  if constexpr (BOX) {   // (the backward pass's; the forward-only instantiation allocates no LDS)
+    for (int e = lane; e < NZ * NZ; e += 64) {
+      const int r = e / NZ, cl = e % NZ;
+      const T wq = (r < NX && cl < NX) ? W.Q[r * NX + cl] : T(0);
+      const T wr = (r >= NX && cl >= NX) ? W.R[(r - NX) * NU + (cl - NX)] : T(0);
+      SW[e] = a.s * (wq + wr);
+    }
+    wave_lds_sync();
+  }
+  // row i of [A|B] at the constant columns (state lanes): position e_p, velocity e_v + h e_p
+  // (h: the tangent's h/6 * 6, above)
+  T crow[6];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    crow[p] = (jx == p) ? T(1) : T(0);
+    crow[3 + p] = ((jx == 6 + p) ? T(1) : T(0)) + ((jx == p) ? h : T(0));
+  }
+
+  M lowm = 0, upm = 0;          // input lanes: active sets of component ju, bit k = stage k
+  bool done = !valid;           // (box: the group has no instance left)
+  int32_t st = MPCB_STATUS_OK;
+  int best = 0x7fffffff, pcount = 3;
+  int n_fwd = 0, n_bst = 0;
+  int kc = -1;                  // highest stage whose active set changed (group-uniform)
+  int git = 0;                  // passes of the group's current instance
+  bool u0fin = true;            // u0 of the flushed (final) pass is finite (staged outputs)
+  const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
+  // an instance's outcome: the QP status of the unconstrained pass (P2 wrote it) carries over
+  auto finish = [&]() {
+    if (valid && j == NX) {
+      bool fin = u0fin;
+      if (!stage_out) {   // direct stores
+        T u0c[NU];
+        load_vec<NU>(a.u0 + b * NU, u0c);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
+      }
+      const int32_t st0 = a.status[b];
+      a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
+      if (BOX && a.qp_stats) {
+        a.qp_stats[2 * b] = n_fwd;
+        a.qp_stats[2 * b + 1] = n_bst;
+      }
+    }
+  };
+#ifdef MPCB_AS_STAMPS
+  unsigned long long ast_prev = __builtin_amdgcn_s_memtime(), ast_acc[12] = {};
+#endif
+  for (;;) {
+#ifdef MPCB_AS_STAMPS
+    ast_acc[8] += 1;
+#endif
+    int kmax = kc;
+#pragma unroll
+    for (int g = 0; g < GROUPS; ++g) {
+      const int o = __builtin_amdgcn_readlane(kc, g * 16);
+      kmax = o > kmax ? o : kmax;
+    }
+    if (git > 0 && !done && kc >= 0) n_bst += kc + 1;
+    if (!done) ++n_fwd;
+    // ------------------------------------------------ masked Riccati over the cached [A|B]
+    ASTAMP(7);
+    if (BOX && kmax >= 0) {   // (a group in its first pass has kc = -1)
+#ifdef MPCB_AS_STAMPS
+      ast_acc[9] += kmax + 1;
+#endif
+      T Pc[NX], pj;
+      {
+        const T vN = stl ? XU.at(N)[jx * SS] - xrN[jx] : T(0);
+        T qn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) qn[i] = stl ? W.QN[i * NX + jx] : T(0);
+        T acc[4] = {T(0), T(0), T(0), T(0)};
+        dot12(acc, vN, qn);
+        pj = stl ? sum4(acc) : T(0);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Pc[i] = qn[i];
+        if (kc >= 0 && kc < N - 1 && stl) {   // restart: the value function stored at kc + 1
+          // P[i][j] sits with lane i at slot (j - i) % 12 when that is <= 6, else with lane j at
+          // slot (i - j) % 12 (the packed PS2 record, mpcb_kernels.h)
+          // (unpacked through the group's LDS block: per-lane LDS offsets instead of 12 global
+          // addresses, which the compiler kept live into a spill)
+          T ps[PS2_W];
+          ldv<T, PS2_W>(PS.at(kc + 1) + jx * PS2_W, ps);
+#pragma unroll
+          for (int d = 0; d < PS2_W; ++d) PX[jx * PS2_W + d] = ps[d];
+          wave_lds_sync();
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            const int dd = (jx - i + NX) % NX;
+            Pc[i] = PX[dd <= 6 ? i * PS2_W + dd : jx * PS2_W + (NX - dd)];
+          }
+          pj = ps[7];
+        }
+        wave_lds_sync();   // the stages' PX writes follow the reads
+      }
+      bool qp_ok = true;
+      // stage data one stage ahead: column j of [A|B], own (ybar - yref) and ybar components,
+      // own gap component
+      // (the prefetch keeps the raw loaded values: forming e = ybar - yref inside it made the
+      // compiler wait for the loads it had just issued, vmcnt(0), at every backward stage)
+      T ncol[NX], nref, nyb, ngp = T(0);
+      auto bload = [&](int k) {
+        // column tv of the stage's ABT2 rows, or (constant directions) of W.ctab: one load
+        // pattern for every lane (no lane branch)
+        const T* rows = tv >= 0 ? ABT.at(k) + tv : W.ctab + cslot;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
+        nyb = XU.at(k)[j * SS];
+        nref = stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju];
+        if (iterate) ngp = GP.at(k)[jx * SS];   // (input lanes: unused)
+      };
+      // (a group loads only the stages it recomputes, k <= kc: the others' results are discarded)
+      if (kmax <= kc) bload(kmax);
+      ASTAMP(0);
+      for (int k = kmax; k >= 0; --k) {
+        const bool act = k <= kc;   // this group's stage is recomputed
+        T col[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) col[i] = ncol[i];
+        const T e = nyb - nref, yb = nyb, gpo = ngp;
+        if (k > 0 && k - 1 <= kc) bload(k - 1);
+        // pt = p + P gap (component j), h = [A|B]^T pt
+        T pt = pj;
+        if (iterate) {
+          T acc[4] = {T(0), T(0), T(0), T(0)};
+          dot12(acc, gpo, Pc);
+          pt += stl ? sum4(acc) : T(0);
+        }
+        T hj;
+        T G[NZ];
+        if constexpr (sizeof(T) == 4) {
+          T acc[4] = {T(0), T(0), T(0), T(0)};
+          dot12(acc, pt, col);
+          hj = sum4(acc);
+          float y[16], g[16];
+          to_columns(outer12(Pc, col), y);   // lane (q,j): Y_q[:, j]  (P symmetric: row = column)
+          to_columns(outer12(col, y), g);    // lane (q,j): G_q[:, j]
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] = g[i];
+        } else {
+          double y[NX], g[NZ];
+          double hh = 0.0;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) y[i] = 0.0;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) g[i] = 0.0;
+          static_for<NX>([&](auto l) { fmac13_bc<decltype(l)::value>(y, hh, Pc, pt, col[l]); });
+#pragma unroll
+          for (int l = 0; l < NX; ++l) fmac16_diag(g, col[l], y[l]);
+          hj = hh;
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] = g[i];
+        }
+        // stage cost: G += s blkdiag(Q, R), h += s blkdiag(Q, R) (ybar - yref)
+        {
+          T swc[NZ];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) swc[i] = SW[i * NZ + j];
+          T acc[4] = {hj, T(0), T(0), T(0)};
+          dot16(acc, e, swc);
+          hj = sum4(acc);
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] += swc[i];
+        }
+        ASTAMP(1);
+        // unmasked input row of a component fixed at this stage: the forward's multiplier.  (Where
+        // the component is free the forward never reads the row, and a stage whose fixed set
+        // changes is recomputed -- and its row written -- before the next forward pass.)
+        {
+          T gr[20];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) gr[i] = G[i];
+          gr[NZ] = hj;
+          gr[17] = gr[18] = gr[19] = T(0);
+          if (act && valid && !stl && (((lowm | upm) >> k) & 1u)) stv<T, 20>(GH.at(k) + ju * 20, gr);
+        }
+        // the 4x4 input block and h_u from the input lanes; masking of the fixed components
+        T Ht[NU * NU], ht[NU], Hux_t[NU];
+        static_for<NU>([&](auto mm) {
+          constexpr int m = decltype(mm)::value;
+          Ht[m * NU + 0] = bc<NX + 0>(G[NX + m]);
+          Ht[m * NU + 1] = bc<NX + 1>(G[NX + m]);
+          Ht[m * NU + 2] = bc<NX + 2>(G[NX + m]);
+          Ht[m * NU + 3] = bc<NX + 3>(G[NX + m]);
+          ht[m] = bc<NX + m>(hj);
+          Hux_t[m] = G[NX + m];
+        });
+        {
+          const bool lo = (lowm >> k) & 1u, hi = (upm >> k) & 1u;
+          const int fx_own = (!stl && (lo || hi)) ? 1 : 0;
+          const T dl_own = lo ? (lbm - yb) : (hi ? (ubm - yb) : T(0));   // input lanes: yb = ubar
+          int fixed[NU];
+          T delta[NU];
+          fixed[0] = bc<NX + 0>(fx_own); fixed[1] = bc<NX + 1>(fx_own);
+          fixed[2] = bc<NX + 2>(fx_own); fixed[3] = bc<NX + 3>(fx_own);
+          delta[0] = bc<NX + 0>(dl_own); delta[1] = bc<NX + 1>(dl_own);
+          delta[2] = bc<NX + 2>(dl_own); delta[3] = bc<NX + 3>(dl_own);
+          T hn[NU];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            T acc = ht[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) acc += fixed[n] ? Ht[m * NU + n] * delta[n] : T(0);
+            hn[m] = fixed[m] ? -delta[m] : acc;
+            Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
+          }
+#pragma unroll
+          for (int m = 0; m < NU; ++m) {
+            ht[m] = hn[m];
+#pragma unroll
+            for (int n = 0; n < NU; ++n) {
+              const bool f = fixed[m] || fixed[n];
+              Ht[m * NU + n] = f ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+            }
+          }
+        }
+        T Lc[10];
+        chol4(Ht, Lc);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) ok = ok && (Lc[i] == Lc[i]);
+        qp_ok = qp_ok && (ok || !act);
+        T kff[NU], Kj[NU], nh[NU];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -ht[m];
+        chol4_solve(Lc, nh, kff);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) nh[m] = -Hux_t[m];
+        chol4_solve(Lc, nh, Kj);
+        T pn = hj;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) pn += G[NX + m] * kff[m];
+        // Pn[i] = G[i] + sum_m H_xu[i][m] K[m][j]; lane i owns H_xu[i][:] = its (unmasked) G[NX..]
+        T Pn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Pn[i] = G[i];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) diag12(Pn, G[NX + m], Kj[m]);
+        {   // KR2: K[m][j] at KR2_W m + j, k_m at KR2_W m + 12
+          if (act && valid) {
+            T* kr = KR.at(k);
+            if (stl) {
+#pragma unroll
+              for (int m = 0; m < NU; ++m) kr[m * KR2_W + j] = Kj[m];
+            } else {
+              kr[ju * KR2_W + 12] = sel<NU>(kff, ju);
+            }
+          }
+        }
+        ASTAMP(2);
+        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
+        if (stl) {
+#pragma unroll
+          for (int i = 0; i < NX; ++i) PX[j * NX + i] = Pn[i];
+        }
+        wave_lds_sync();
+        {
+          const uint64_t ma = lane_mask(act);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            const T o = PX[i * NX + jx];
+            const T nv = csel(mst, csel(lane_mask(i <= j), Pn[i], o), T(0));
+            Pc[i] = csel(ma, nv, Pc[i]);
+          }
+          pj = csel(ma, csel(mst, pn, T(0)), pj);
+        }
+        // packed snapshot of P_k, p_k for a later restart: slot d of lane j is P[j][(j + d) % 12],
+        // the entry lane max(j, o) published above
+        {
+          T ps[PS2_W];
+#pragma unroll
+          for (int d = 0; d < 7; ++d) {
+            const int o = jx + d < NX ? jx + d : jx + d - NX;
+            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
+          }
+          ps[7] = pj;
+          if (act && valid && stl && k > 0) stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);
+        }
+        wave_lds_sync();
+        ASTAMP(3);
+      }
+      if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
+    }
+
+    // ------------------------------------------------ forward pass, multipliers, violations
+    M vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
+    const bool write = valid && !done;
+    // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
+    T* const xs = reinterpret_cast<T*>(as_dyn) + q * out_elems<T>(N);   // X rows, then U rows
+    T* const us = xs + (N + 1) * NX;
+    T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
+    if (iterate && stl) zj = a.x0[b * a.x0_sb + jx] - XU.at(0)[jx * SS];
+    // Stage data FD stages ahead in a ring of register slots (the stage loop is unrolled by FD so
+    // every slot is a fixed register set, loaded at the end of the stage that consumed it and used
+    // FD - 1 stages later): own ybar component; one row (a state lane's ABT2 row: the variable
+    // columns of row jx of [A|B] and the gap; an input lane's KR2 row: row ju of K and k_ju);
+    // input lanes whose component is fixed
+    // at the stage: row ju of the stage Hessian with h_u.  The raw vectors stay in the slot until
+    // use: moving them on arrival would make the compiler wait for the loads right away.
+    // (The Hessian rows, needed at few stages, come one stage ahead through a single slot.)
+    constexpr int FD = BOX ? MPCB_AS_FDEPTH : MPCB_FWD_FDEPTH;
+    constexpr int FL = KR2_W;
+    T pv[FD][FL], pyb[FD], pgp[FD], pg[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) pg[i] = T(0);   // (a free component's row is never loaded)
+    auto rload = [&](int k, auto slot_tag) {
+      constexpr int sl = decltype(slot_tag)::value;
+      pyb[sl] = XU.at(k)[j * SS];
+      // one load for both kinds of lane, from a per-lane address: an input lane's KR2 row (13
+      // elements used), a state lane's 10-element ABT2 row followed by the next row or record,
+      // or by the workspace padding; 8-B vectors in fp32 (rows start 8-B aligned), 16-B in fp64
+      ldv<T, FL, sizeof(T) == 8 ? 16 : 8>(stl ? ABT.at(k) + jx * ABT2_W : KR.at(k) + ju * KR2_W, pv[sl]);
+      if (iterate) pgp[sl] = GP.at(k)[jx * SS];   // state lanes: gap_jx (input lanes: unused)
+    };
+    auto gload = [&](int k) {
+      // (the 17 used elements only: loading the row's 3 pad elements too left registers the
+      // compiler reused as temporaries while the load was in flight -- a vmcnt(0) wait per stage)
+      if (BOX && (((lowm | upm) >> k) & 1u)) {
+        ldv<T, 16>(GH.at(k) + ju * 20, pg);
+        pg[NZ] = GH.at(k)[ju * 20 + NZ];
+      }
+    };
+    // a converged group rides along with its wave's other groups: its loads are skipped and its
+    // results (garbage) neither written nor used
+    const bool fetch = !BOX || !done;
+    if (fetch) gload(0);
+    static_for<FD>([&](auto s) { rload(decltype(s)::value < N ? decltype(s)::value : N - 1, s); });
+    auto stage = [&](int k, auto slot_tag) {
+      constexpr int sl = decltype(slot_tag)::value;
+      // the lane's row of the dot below: a state lane's row of [A|B] (variable columns loaded,
+      // constant ones crow); an input lane's row of the stage Hessian with h_u (box), loaded where
+      // its component is fixed -- elsewhere the multiplier it yields is never read, so the row
+      // is whatever the slot held (no select on the fixed set), and without the box the input
+      // lanes' dot result is not used at all (no selects)
+      T row[NZ];
+      if constexpr (BOX) {
+#pragma unroll
+        for (int t = 0; t < NVAR; ++t) row[var_col(t)] = csel(mst, pv[sl][t], pg[var_col(t)]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          row[p] = csel(mst, crow[p], pg[p]);
+          row[6 + p] = csel(mst, crow[3 + p], pg[6 + p]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NVAR; ++t) row[var_col(t)] = pv[sl][t];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          row[p] = crow[p];
+          row[6 + p] = crow[3 + p];
+        }
+      }
+      const T r0 = csel(mst, iterate ? pgp[sl] : T(0), BOX ? pg[NZ] : T(0));
+      const T yb = pyb[sl];
+      ASTAMP(4);
+      // du = k + K dx (input lanes; dx_i broadcast from state lane i)
+      {
+        T acc[4] = {pv[sl][NX], T(0), T(0), T(0)};
+        T krow[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) krow[i] = pv[sl][i];
+        dot12(acc, zj, krow);
+        zj = csel(mst, zj, sum4(acc));
+      }
+      const T yo = yb + zj;   // state lanes: x_k = xbar_k + dx_k; input lanes: u_k
+      if (stage_out) {
+        if (stl) xs[k * NX + jx] = yo;
+        else us[k * NU + ju] = yo;
+      } else if (write) {
+        if (stl) {
+          if (a.X) a.X[(b * (N + 1) + k) * NX + jx] = yo;
+        } else {
+          if (a.U) a.U[(b * N + k) * NU + ju] = yo;
+          if (k == 0) a.u0[b * NU + ju] = yo;
+        }
+      }
+      ASTAMP(5);
+      // every lane: r0 + row . z  (state lanes dx_{k+1}; input lanes the multiplier mu)
+      T acc[4] = {r0, T(0), T(0), T(0)};
+      dot16(acc, zj, row);
+      const T v = sum4(acc);
+      const bool lo = !stl && ((lowm >> k) & 1u), hi = !stl && ((upm >> k) & 1u);
+      T tol_mu = T(0);
+      if (BOX && __builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
+        T aa[4] = {T(fabs(r0)), T(0), T(0), T(0)};
+        dot16abs(aa, zj, row);
+        tol_mu = T(64) * eps * sum4(aa);
+      }
+      if (!stl) {
+        const bool fr = !(lo || hi);
+        const T mu = v;
+        // violations beyond the rounding noise of u and mu (see mpcb_box.hip)
+        vlo |= (M)(fr && yo < lbm - tol_u) << k;
+        vhi |= (M)(fr && yo > ubm + tol_u) << k;
+        vfl |= (M)(lo && mu < -tol_mu) << k;
+        vfu |= (M)(hi && mu > tol_mu) << k;
+      } else {
+        zj = v;
+      }
+      // the next stage's Hessian rows (fixed components only), then this slot's refill FD stages
+      // ahead from every lane (the tail reloads stage N - 1, unused): in this order the waits for
+      // both stay exact
+      if (k + 1 < N && fetch) gload(k + 1);
+      rload(k + FD < N ? k + FD : N - 1, slot_tag);
+      ASTAMP(6);
+    };
+    if constexpr (!BOX) AS_WT(1);
+    for (int k0 = 0; k0 < N; k0 += FD) {
+      static_for<FD>([&](auto s) {
+        if (k0 + decltype(s)::value < N) stage(k0 + decltype(s)::value, s);
+      });
+    }
+    if constexpr (!BOX) AS_WT(2);
+    // outputs of this pass: staged rows leave as 16-B vectors once the pass is known to be final
+    // (the unconstrained pass; the active-set pass that converged or used the last iteration)
+    if (stage_out && stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
+    auto flush_out = [&]() {
+      wave_lds_sync();
+      constexpr int V = 16 / sizeof(T);
+      typedef T Vec __attribute__((ext_vector_type(V)));
+      const int nx = (N + 1) * NX, nu = N * NU;
+      if (a.X) {
+        Vec* dst = reinterpret_cast<Vec*>(a.X + b * nx);
+        const Vec* src = reinterpret_cast<const Vec*>(xs);
+        for (int t = j; t < nx / V; t += NZ) dst[t] = src[t];
+      }
+      if (a.U) {
+        Vec* dst = reinterpret_cast<Vec*>(a.U + b * nu);
+        const Vec* src = reinterpret_cast<const Vec*>(us);
+        for (int t = j; t < nu / V; t += NZ) dst[t] = src[t];
+      }
+      if (!stl) a.u0[b * NU + ju] = us[ju];
+      u0fin = true;
+#pragma unroll
+      for (int m = 0; m < NU; ++m) u0fin = u0fin && isfin(us[m]);
+    };
+    if (!stage_out && write && a.X && stl) a.X[(b * (N + 1) + N) * NX + jx] = XU.at(N)[jx * SS] + zj;
+    if (!BOX && stage_out && write) flush_out();
+    if constexpr (!BOX) break;
+
+    // ------------------------------------------------ active-set update (Kim-Park)
+    const M V = vlo | vhi | vfl | vfu;
+    const int cnt = stl ? 0 : Mk::popc(V);
+    const int firstk = (!stl && V) ? Mk::ffs(V) - 1 : WB;
+    int nV, first;
+    {
+      const int c0 = bc<NX + 0>(cnt), c1 = bc<NX + 1>(cnt), c2 = bc<NX + 2>(cnt), c3 = bc<NX + 3>(cnt);
+      nV = (c0 + c1) + (c2 + c3);
+      const int f0 = bc<NX + 0>(firstk) * NU + 0, f1 = bc<NX + 1>(firstk) * NU + 1;
+      const int f2 = bc<NX + 2>(firstk) * NU + 2, f3 = bc<NX + 3>(firstk) * NU + 3;
+      const int fa = f0 < f1 ? f0 : f1, fb = f2 < f3 ? f2 : f3;
+      first = fa < fb ? fa : fb;
+    }
+    const bool gconv = nV == 0;
+    const bool full = (nV < best) || (pcount > 0);
+    pcount = (nV < best) ? 3 : (full ? pcount - 1 : pcount);
+    best = nV < best ? nV : best;
+    const M selm = full ? V : ((first < WB * NU && (first % NU) == ju && !stl) ? (M(1) << (first / NU)) : M(0));
+    const M nlow = (lowm | (selm & vlo)) & ~(selm & vfl);
+    const M nup = (upm | (selm & vhi)) & ~(selm & vfu);
+    const M diff = stl ? M(0) : ((nlow ^ lowm) | (nup ^ upm));
+    M changed = (bc<NX + 0>(diff) | bc<NX + 1>(diff)) | (bc<NX + 2>(diff) | bc<NX + 3>(diff));
+    if (!done && !gconv) {
+      lowm = nlow;
+      upm = nup;
+    } else {
+      changed = 0;
+    }
+    // restart at kc + 1 from the snapshot there: the last pass that recomputed that stage, or
+    // (never recomputed: its active set is still empty) P2's unconstrained pass
+    kc = changed ? WB - 1 - Mk::clz(changed) : -1;
+    // the instance is finished: converged, or the pass cap
+    const bool fin_now = write && (gconv || git + 1 >= a.max_as_iter);
+    if (stage_out && fin_now) flush_out();
+    wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
+    ++git;
+    if (fin_now) {
+      if (!gconv) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+      finish();
+      // the next instance of the chunk (lane 0 of the group draws it), else the group stays empty
+      int nxt = (int)nb;
+      if (a.as_queue) {
+        if (j == 0) nxt = (int)gridDim.x * GROUPS + atomicAdd(a.as_queue, 1);
+        nxt = bc<0>(nxt);
+      }
+      bind(nxt);
+      lowm = upm = 0;
+      st = MPCB_STATUS_OK;
+      best = 0x7fffffff;
+      pcount = 3;
+      n_fwd = n_bst = 0;
+      kc = -1;
+      git = 0;
+      u0fin = true;
+      done = !valid;
+    } else if (!valid) {
+      done = true;
+    }
+    if (__all(done)) break;
+  }
+#ifdef MPCB_AS_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
+#endif
+  if constexpr (!BOX) finish();   // (the box kernel finishes each instance as it converges)
+  if constexpr (!BOX) AS_WT(3);
+}
+
+}  // namespace asq
+}  // namespace mpcb

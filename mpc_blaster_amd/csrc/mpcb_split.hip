@@ -69,6 +69,7 @@ WT_TABLE(g_wt_p1)
 }  // namespace mpcb
 
 #include "mpcb_row.h"
+#include "mpcb_as.h"
 
 namespace mpcb {
 
@@ -1117,6 +1118,24 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_kernel(SplitArgs
   riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
+// ... and the forward pass of the quad too (MPCB_FUSE_FWD=1): the waves that finish their
+// Riccati recursion early stream their forward pass while the slow ones still factorise.
+// Measured at c2: 0.0986-0.1003 vs 0.1003-0.1007 ms with fwd_rm as its own launch, within the
+// run-to-run spread, so off (fwd_rm keeps its own launch and roofline line)
+#ifndef MPCB_FUSE_FWD
+#define MPCB_FUSE_FWD 0
+#endif
+template <bool ITER, bool DJ>
+__global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_fwd_kernel(SplitArgs<double> a) {
+  row_body<double, ITER, DJ, true>(a);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  asq::as_body<double, false, false, ITER>(a);
+}
+
 template <class T, bool USE_CC, bool ITER>
 static hipError_t launch_forward_m(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
   constexpr size_t bytes = FwdLds<T, USE_CC>::BYTES;
@@ -1139,14 +1158,27 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
   const bool fuse = sizeof(T) == 8 && MPCB_FUSE_P12 && a.quad_p1 == 2 && a.tin == 1 && !a.small;
+  const bool fuse3 = fuse && MPCB_FUSE_FWD && a.fwd && a.fwd16 && !a.GH;
   if (fuse) {
     // (the phase events: "nominal" empty, "riccati" the fused kernel)
     if (ev) (void)hipEventRecord(ev[1], st);
     const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
-    const size_t lds = row_lds_bytes(a);
+    size_t lds = row_lds_bytes(a);
     const bool it = a.mode == MPCB_MODE_ITERATE;   // (the row body's mode is always a template argument)
     if constexpr (sizeof(T) == 8) {
-      if (row_dj(a)) {
+      if (fuse3) {
+        const size_t lo = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
+        lds = lds > lo ? lds : lo;   // (the two bodies' dynamic LDS alias: one after the other)
+        const bool it3 = MPCB_AS_ITER_T && it;
+        if (!it3 && it) return hipErrorInvalidValue;   // (built with the mode as a template argument)
+        if (row_dj(a)) {
+          if (it3) hipLaunchKernelGGL((row_riccati_fwd_kernel<true, true>), grid, dim3(64), lds, st, a);
+          else hipLaunchKernelGGL((row_riccati_fwd_kernel<false, true>), grid, dim3(64), lds, st, a);
+        } else {
+          if (it3) hipLaunchKernelGGL((row_riccati_fwd_kernel<true, false>), grid, dim3(64), lds, st, a);
+          else hipLaunchKernelGGL((row_riccati_fwd_kernel<false, false>), grid, dim3(64), lds, st, a);
+        }
+      } else if (row_dj(a)) {
         if (it) hipLaunchKernelGGL((row_riccati_kernel<true, true>), grid, dim3(64), lds, st, a);
         else hipLaunchKernelGGL((row_riccati_kernel<false, true>), grid, dim3(64), lds, st, a);
       } else {
@@ -1201,7 +1233,9 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
   // back from HBM.
   hipError_t e = hipSuccess;
-  if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_as.hip)
+  if (fuse3) {
+    // (the forward pass ran in row_riccati_fwd_kernel)
+  } else if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_as.hip)
     e = launch_as<T>(a, st);
   else if (a.fwd && a.fwd16)   // forward pass from the exported [A|B]^T, 16 lanes per instance
     e = launch_fwd_rm<T>(a, st);
