@@ -36,7 +36,14 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 // table, s_memrealtime (100 MHz, one clock for the whole chip) at slot 0 entry, 1 loop start,
 // 2 loop end, 3 exit; lane 0 of each of the first 4096 workgroups writes it (a vector store).
 #ifdef MPCB_STAMPS
-#define WT_TABLE(name) __device__ unsigned long long name[4096 * 4];
+#define WT_TABLE(name) __device__ unsigned long long name[4096 * 5];
+// slot 4 of the table (entries 4096 * 4 + wg): the wave's HW_ID (SIMD, CU, SE) and XCC_ID
+#define WT_HW(name)                                                                 \
+  {                                                                                 \
+    const unsigned hw_ = __builtin_amdgcn_s_getreg(63492), xcc_ = __builtin_amdgcn_s_getreg(63508); \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                               \
+      name[4096 * 4 + blockIdx.x] = ((unsigned long long)xcc_ << 32) | hw_;        \
+  }
 #define WT(name, slot)                                                              \
   {                                                                                 \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
@@ -45,6 +52,7 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 #else
 #define WT_TABLE(name)
 #define WT(name, slot)
+#define WT_HW(name)
 #endif
 
 // f(std::integral_constant<int, i>{}) for i = 0 .. n-1 (compile-time lane indices for DPP)

@@ -474,6 +474,7 @@ WT_TABLE(g_wt_p2)
 template <class T, bool EXPORT, bool ITER = false, bool TIN = false>
 __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   WT(g_wt_p2, 0);
+  WT_HW(g_wt_p2);
   // fp64 DPP path: every exchange of the stage by row broadcasts -- Y reads P straight out of
   // the lanes' unsymmetrised columns (lane max(i, l) owns entry (i, l): mpcb_dpp_gen.h ypn_bc),
   // the stage-cost term S v, H_uu and h_u by broadcasts -- so P needs no LDS transpose and the
@@ -1256,10 +1257,10 @@ template int64_t split_elems_per_instance<float>(int, int, int);
 // (same translation unit as g_stamps: the library is built without -fgpu-rdc)
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p1f(unsigned long long* out) {   // the row body inside row_riccati_kernel
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
 }
 extern "C" int mpcb_debug_wt_p2(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * 4096 * 4) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
 }
 #endif
 extern "C" int mpcb_debug_stamps(unsigned long long* out) {

@@ -29,12 +29,14 @@ waves = B // 4
 starts = {}
 # (c2 runs P1 inside row_riccati_kernel: its table is p1f; MPCB_FUSE_P12=0 builds: p1)
 for name in ('p1f' if os.environ.get('WT_P1', 'p1f') == 'p1f' else 'p1', 'p2', 'p3'):
-    buf = (ctypes.c_ulonglong * (4096 * 4))()
+    buf = (ctypes.c_ulonglong * (4096 * 5))()
     f = getattr(lib, f'mpcb_debug_wt_{name}')
     name = name[:2]
     f.argtypes = [ctypes.c_void_p]
     assert f(buf) == 0
-    t = np.array(buf, dtype=np.float64).reshape(4096, 4)[:waves] * 0.01   # us
+    raw = np.array(buf, dtype=np.uint64)
+    hw = raw[4096 * 4:4096 * 4 + waves]
+    t = raw[:4096 * 4].astype(np.float64).reshape(4096, 4)[:waves] * 0.01   # us
     t0 = t[:, 0].min()
     starts[name] = (t0, t[:, 3].max())
     r = t - t0
@@ -45,6 +47,18 @@ for name in ('p1f' if os.environ.get('WT_P1', 'p1f') == 'p1f' else 'p1', 'p2', '
           f'exits p50 {np.percentile(r[:, 3], 50):6.2f} max {r[:, 3].max():6.2f}')
     if name == 'p2':
         lp = r[:, 2] - r[:, 1]
+        hid = hw & 0xFFFFFFFF
+        simd = (hid >> 4) & 3
+        cu = (hid >> 8) & 15
+        sh = (hid >> 12) & 1
+        se = (hid >> 13) & 7
+        xcc = (hw >> 32) & 15
+        key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
+        _, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+        share = cnt[inv]   # waves of this kernel on the same SIMD
+        print('   p2 waves per SIMD: ', np.bincount(share).tolist(), '| loop median when alone',
+              round(float(np.median(lp[share == 1])), 2), 'shared',
+              round(float(np.median(lp[share > 1])), 2) if (share > 1).any() else None)
         xcd = np.arange(waves) % 8
         print('   p2 loop by blockIdx % 8:', ' '.join(f'{np.median(lp[xcd == x]):5.2f}' for x in range(8)),
               '| slowest 5% by XCD:', np.bincount(xcd[lp > np.percentile(lp, 95)], minlength=8).tolist())
