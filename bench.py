@@ -27,15 +27,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-FLOP_PER_INTERVAL = 34785          # dense algorithmic flops per shooting interval
-# the Riccati kernel (dominant): RK4 sensitivities (21,996) minus the 4 f evaluations the nominal
-# pass already did (4 x 300), plus the Riccati backward recursion (12,309)
-FLOP_PER_INTERVAL_RICCATI = 21996 - 4 * 300 + 12309
-# fp64 chunks <= 16384 (c2): the row rollout integrates the sensitivities itself and exports [A|B]
-# (mpcb_rollout.hip, SplitArgs::tin), so it carries the whole RK4 + sensitivity count and P2 the
-# Riccati backward alone
-FLOP_PER_INTERVAL_ROLLOUT_TAN = 21996
-FLOP_PER_INTERVAL_RICCATI_TIN = 12309
+# dense algorithmic flops per shooting interval: per phase kernel in kernel_flops
 PEAK_TFLOPS = {'f64': 78.6, 'f32': 157.3}   # MI355X dense vector (= matrix) peaks, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 
@@ -238,61 +230,67 @@ def run(w, world, rank, dev, steps, warmup, stub=None, dump_gather=None):
             t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=odev)
             dist.all_reduce(t)
             qp['fwd_passes'], qp['bwd_stages'] = float(t[0]) / world, float(t[1]) / world
-    two = w['batch'] <= 16384 and w['dtype'] == 'f64'   # P1 + P2 in one launch (row_riccati_kernel)
-    path = (('split (2 kernels: rollout+Riccati, forward)' if two else 'split (3 kernels)')
-            if mpc.path == 'split' else 'fused (1 kernel)')
+    # the kernels the timed solves launched, as rocprof names them (mpcb_last_kernels), checked
+    # against the device-free plan of the same config (mpcb_plan_kernels) that the CPU tests pin
+    # to the committed PMC summaries
+    kernels = mpc.last_kernels()
+    if cuda:
+        plan = mpc.plan_kernels(B, want_traj=traj)
+        if plan != kernels:
+            raise SystemExit(f'launched kernels {kernels} differ from the plan {plan}')
+    path = ' + '.join(kernels[k] for k in ('nominal', 'riccati', 'linearise', 'forward') if k in kernels)
     mpc.close()
     return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path, phase_ms=phase_ms,
-                split=path.startswith('split'), qp=qp)
+                kernels=kernels, split=mpc.path == 'split', qp=qp, cuda=cuda)
 
 
 def phase_kernels(w):
-    """rocprof names and algorithmic flop counts of the split path's three launches for this
-    workload (the library picks the variants by chunk size: mpcb_capi.hip mpcb_create).
-    Dense algorithmic counts per shooting interval:
-      nominal  4 f evaluations (4 x 300) of the RK4 rollout; with the tangent export (fp64 chunks
-               <= 16384: c2) the RK4 rollout and its sensitivities, 21,996;
-      riccati  RK4 sensitivities minus those f evaluations plus the Riccati backward
-               (21,996 - 1,200 + 12,309 = 33,105); with the tangent export (c2) P1 and P2 are ONE
-               launch per quad (row_riccati_kernel), the rollout with sensitivities plus the
-               Riccati backward, 21,996 + 12,309 = 34,305, and the "nominal" phase is empty;
-      forward  du = K dx + k, dx' = [A|B] (dx, du) (+ gap): 480;
-      box      the active-set kernel (c4): per masked backward stage recomputed 12,309 (the Riccati
-               algebra over the cached [A|B]), per forward stage 480 + the multipliers
-               mu = G_u (dx, du) + h_u (2 x 17 x 4 = 136), counted from the kernel's own per-instance
-               statistics (mpcb_qp_stats) rather than assumed.
+    """{phase: rocprof kernel name} of the solve this workload times: the library's own plan for
+    the bench's handle (mpcb_plan_kernels: the selection code of mpcb_create / mpcb_solve, run
+    without a device), so the roofline names exactly the dispatch rocprof and the PMC summary
+    record (run() also checks the plan against what the timed solves launched)."""
+    from mpc_blaster_amd import MPCConfig, _lib
+    box = w['box']
+    cfg = MPCConfig(N=w['N'], dtype=w['dtype'], lbu=np.zeros(4) if box else None,
+                    ubu=np.full(4, 65.0) if box else None, max_as_iter=w.get('max_as_iter', 200))
+    return _lib.plan_kernels(cfg.to_c(), w['batch'], w['batch'], want_traj=not w['hist'])
+
+
+def kernel_flops(w, r, phase, kernel):
+    """Dense algorithmic flops (per shooting interval) of one phase's kernel:
+      nominal_row_kernel<T, ITER, DJ, true>  the RK4 rollout with its sensitivities, 21,996
+      other rollouts (nominal_*)             4 f evaluations, 4 x 300 = 1,200
+      row_riccati_kernel                     the rollout with sensitivities AND the Riccati
+                                             backward of the same quad, 21,996 + 12,309 = 34,305
+      riccati_kernel_*<E, ITER, true>        the Riccati backward over the rollout's [A|B], 12,309
+      riccati_kernel_* (captured scalars)    the sensitivities minus the rollout's 4 f evaluations
+                                             plus the Riccati backward, 21,996 - 1,200 + 12,309 = 33,105
+      as_kernel_*                            the active set (c4): per masked backward stage
+                                             recomputed 12,309, per forward stage 480 + the
+                                             multipliers mu = G_u (dx, du) + h_u (136), counted from
+                                             the kernel's own statistics (mpcb_qp_stats)
+      fwd_rm_kernel / forward_kernel         du = K dx + k, dx' = [A|B] (dx, du) (+ gap): 480
     """
-    t = 'float' if w['dtype'] == 'f32' else 'double'
-    small = w['batch'] <= 16384
-    tin = small and w['dtype'] == 'f64'
-    if tin:   # P1 and P2 in one kernel per quad (mpcb_split.hip row_riccati_kernel, MPCB_FUSE_P12)
-        return {'riccati': 'row_riccati_kernel<false, true>', 'forward': f'fwd_rm_kernel<{t}, false>'}
-    # (the rollout-mode instantiations: the mode is a template argument of P1, P2 and P3; the row
-    # rollout's <T, ITER, DJ, TAN>: DJ = the reference's diagonal inertia)
-    names = {'nominal': f'nominal_row_kernel<{t}, false, true, {"true" if tin else "false"}>' if small
-             else f'nominal_kernel<{t}, false>',
-             'riccati': f'riccati_kernel_{w["dtype"]}<{"true" if (w["box"] or w["dtype"] == "f64" or (small and not w["hist"])) else "false"}, false'
-                        + (', true>' if tin else '>')}
-    if w['box']:   # the row-major active-set kernel (mpcb_as.hip)
-        # (as_kernel_*<true>: the 32-bit stage masks of N <= 32, mpcb_as.hip launch_as)
-        names['forward'] = f'as_kernel_{w["dtype"]}<{"true" if w["N"] <= 32 else "false"}, false>'
-    elif not w['hist']:   # small chunks: the DPP forward pass over P2's row-major exports
-        names['forward'] = f'fwd_rm_kernel<{t}, false>' if small else f'forward_kernel<{t}, false, false>'
-    return names
-
-
-def kernel_flops(w, r, phase):
     B, N = w['batch'], w['N']
-    tin = B <= 16384 and w['dtype'] == 'f64'
-    if phase == 'nominal':
-        return (FLOP_PER_INTERVAL_ROLLOUT_TAN if tin else 1200) * N * B
-    if phase == 'riccati':   # (tin: the fused rollout + Riccati kernel)
-        return ((FLOP_PER_INTERVAL_ROLLOUT_TAN + FLOP_PER_INTERVAL_RICCATI_TIN) if tin
-                else FLOP_PER_INTERVAL_RICCATI) * N * B
-    if w['box']:
+    name = kernel.split('::')[-1]
+    base, targs = (name.split('<', 1) + [''])[:2]
+    last_true = targs.rstrip('>').split(',')[-1].strip() == 'true'
+    if base == 'nominal_row_kernel':
+        per = 21996 if last_true else 1200
+    elif base.startswith('nominal'):
+        per = 1200
+    elif base == 'row_riccati_kernel':
+        per = 21996 + 12309
+    elif base.startswith('riccati_kernel') or base == 'riccati':   # ('riccati': the CPU stub's)
+        per = 12309 if last_true else 21996 - 1200 + 12309
+    elif base.startswith('as_kernel'):
         q = r['qp']
         return 12309 * q['bwd_stages'] + (480 + 136) * N * q['fwd_passes']
-    return 480 * N * B
+    elif base in ('fwd_rm_kernel', 'forward_kernel', 'forward'):
+        per = 480
+    else:
+        raise SystemExit(f'no flop count for kernel {kernel} (phase {phase})')
+    return per * N * B
 
 
 def dispatches_per_phase(B: int) -> int:
@@ -315,18 +313,17 @@ def kernel_bytes(w, r, phase):
 
 
 def pmc_kernel(workload: str, kernel: str):
-    """Counter-derived figures of one kernel from the committed PMC summary (tools/pmc_summary.py)."""
+    """Counter-derived figures of one kernel from the committed PMC summary (tools/pmc_summary.py).
+    A committed summary without an entry for the kernel is an error, not a null: the roofline
+    would cite a profile of some other kernel."""
     p = os.path.join(REPO, 'profiles', f'pmc_{workload}.json')
     if not os.path.exists(p):
         return None
-    try:
-        per = json.load(open(p)).get('per_kernel', {})
-    except Exception:
-        return None
-    for k, v in per.items():
-        if k.endswith('::' + kernel) or k == kernel:
-            return v
-    return None
+    per = json.load(open(p)).get('per_kernel', {})
+    if kernel not in per:
+        raise SystemExit(f'{p} has no entry for the dominant kernel {kernel} (it holds {sorted(per)}): '
+                         're-collect it (tools/collect_profiles.sh)')
+    return per[kernel]
 
 
 def summarize(w, r, world, steps):
@@ -336,15 +333,15 @@ def summarize(w, r, world, steps):
     ph = r['phase_ms']
     if not r['split']:
         raise RuntimeError('bench expects the split path')
-    names = phase_kernels(w)
+    names = r['kernels']
     # the dominant kernel by device time (HIP events on its launch stream)
     dom = max(names, key=lambda k: ph.get(k, 0.0))
-    flop = kernel_flops(w, r, dom)
+    flop = kernel_flops(w, r, dom, names[dom])
     achieved_tf = flop / (ph[dom] * 1e-3) / 1e12
-    solve_flop = sum(kernel_flops(w, r, k) for k in names)
+    solve_flop = sum(kernel_flops(w, r, k, names[k]) for k in names)
     solve_tf = solve_flop / (r['kern_ms'] * 1e-3) / 1e12
     hbm_gbs = compulsory_bytes(w) * B / (r['kern_ms'] * 1e-3) / 1e9
-    pk = pmc_kernel(w['name'], names[dom]) or {}
+    pk = (pmc_kernel(w['name'], names[dom]) if r['cuda'] else None) or {}
     # the library launches each phase once per chunk of instances (mpcb_capi.hip mpcb_create:
     # 65536, MPCB_CHUNK); the PMC summary is per dispatch, the phase time and the flop count per
     # phase, so the counter figures are scaled to the phase (c5: 131072 = 2 dispatches)
@@ -360,7 +357,7 @@ def summarize(w, r, world, steps):
             'flop_per_phase': flop, 'executed_flop_per_phase': ex,
             'executed_frac': (ex / (ph[dom] * 1e-3) / 1e12 / peak) if ex else None,
             'phase_ms': ph, 'phase_kernels': names,
-            'phase_frac': {k: kernel_flops(w, r, k) / (ph[k] * 1e-3) / 1e12 / peak
+            'phase_frac': {k: kernel_flops(w, r, k, names[k]) / (ph[k] * 1e-3) / 1e12 / peak
                            for k in names if ph.get(k, 0) > 0},
             'solve_ms': r['kern_ms'],
             'solve_achieved': solve_tf,

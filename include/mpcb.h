@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MPCB_ABI_VERSION 4
+#define MPCB_ABI_VERSION 5
 
 enum { MPCB_F64 = 0, MPCB_F32 = 1 };
 enum { MPCB_MODE_ROLLOUT = 0, MPCB_MODE_ITERATE = 1 };
@@ -104,6 +104,18 @@ int mpcb_path(const mpcb_handle* h);
  * No reference counterpart (acados' ``get_stats('time_tot')`` is host wall time). */
 int mpcb_set_timing(mpcb_handle* h, int enable);
 int mpcb_last_timing(mpcb_handle* h, float ms[3]);
+/* Kernels of a solve, one line per timing phase (the slots of mpcb_last_timing: nominal, Riccati,
+ * forward pass / 17/6 linearisation; a fourth line for the small-chunk path's linearisation),
+ * as rocprofv3 names the dispatches ("mpcb::riccati_kernel_f32<false, false, false>"), an empty
+ * line for a phase without a launch; NUL-terminated in buf[len].
+ * mpcb_plan_kernels: what mpcb_solve (mode MPCB_MODE_ROLLOUT, want_traj: X and U requested) or
+ * mpcb_solve_iterate (MPCB_MODE_ITERATE) of B instances would launch on a handle created with
+ * (cfg, max_batch) -- the same selection code, run without a device (no HIP call).
+ * mpcb_last_kernels: what the handle's last solve launched.
+ * No reference counterpart (profiling aid: ties a roofline to the rocprof dispatch it cites). */
+int mpcb_plan_kernels(const mpcb_config* cfg, int64_t max_batch, int64_t B, int mode, int want_traj,
+                      char* buf, int64_t len);
+int mpcb_last_kernels(const mpcb_handle* h, char* buf, int64_t len);
 
 /*
  * One SQP_RTI step for B independent instances, linearised at the RK4 rollout of u_ref from

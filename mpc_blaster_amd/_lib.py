@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = 'libmpcblaster.so'
 LIB_PATH = os.path.join(_HERE, LIB_NAME)
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MPCB_F64, MPCB_F32 = 0, 1
 MPCB_MAX_NX, MPCB_MAX_NU = 17, 6
 STATUS_OK, STATUS_NAN, STATUS_MAXITER, STATUS_MINSTEP, STATUS_QP_FAIL = 0, 1, 2, 3, 4
@@ -21,7 +21,11 @@ EXPORTS = ('mpcb_create', 'mpcb_destroy', 'mpcb_last_error', 'mpcb_abi_version',
            'mpcb_workspace_bytes', 'mpcb_path', 'mpcb_solve', 'mpcb_solve_iterate', 'mpcb_linearize',
            'mpcb_sim_step', 'mpcb_gen_inputs', 'mpcb_histogram', 'mpcb_set_timing',
            'mpcb_last_timing', 'mpcb_set_params', 'mpcb_set_t_blast', 'mpcb_qp_stats', 'mpcb_poc_jacobians',
-           'mpcb_quat_ops')
+           'mpcb_quat_ops', 'mpcb_plan_kernels', 'mpcb_last_kernels')
+# the timing / launch-log slots of the split path (mpcb_last_timing, mpcb_plan_kernels) and of the
+# 17/6 model
+PHASES_12 = ('nominal', 'riccati', 'forward', 'linearise')
+PHASES_17 = ('nominal', 'riccati', 'linearise', '')
 
 
 class MpcbConfig(ctypes.Structure):
@@ -86,6 +90,8 @@ def load(path: str | None = None):
     lib.mpcb_poc_jacobians.argtypes = [i64, vp, dbl, ctypes.POINTER(dbl), i32, dbl, vp, vp, vp, vp, vp,
                                        vp, vp]
     lib.mpcb_quat_ops.argtypes = [i64, vp, vp, vp, vp, vp, vp]
+    lib.mpcb_plan_kernels.argtypes = [ctypes.POINTER(MpcbConfig), i64, i64, i32, i32, ctypes.c_char_p, i64]
+    lib.mpcb_last_kernels.argtypes = [vp, ctypes.c_char_p, i64]
     for name in EXPORTS:
         if name not in ('mpcb_last_error', 'mpcb_workspace_bytes'):
             getattr(lib, name).restype = i32
@@ -102,6 +108,25 @@ def load(path: str | None = None):
 
 class MpcbError(RuntimeError):
     pass
+
+
+def kernel_names(fill, full: bool) -> dict:
+    """{phase: rocprof kernel name} from mpcb_plan_kernels / mpcb_last_kernels (``fill(buf, len)``
+    calls one of them), phases without a launch omitted."""
+    buf = ctypes.create_string_buffer(4096)
+    check(fill(buf, len(buf)))
+    names = buf.value.decode().split('\n')
+    keys = PHASES_17 if full else PHASES_12
+    return {k: n for k, n in zip(keys, names) if k and n}
+
+
+def plan_kernels(cfg: MpcbConfig, max_batch: int, B: int, iterate: bool = False, want_traj: bool = True) -> dict:
+    """The kernels a handle of (cfg, max_batch) launches for a solve of B instances, without a
+    device (include/mpcb.h mpcb_plan_kernels)."""
+    lib = load()
+    return kernel_names(lambda b, n: lib.mpcb_plan_kernels(ctypes.byref(cfg), int(max_batch), int(B),
+                                                           1 if iterate else 0, 1 if want_traj else 0, b, n),
+                        cfg.nx == 17)
 
 
 def check(rc: int):

@@ -77,6 +77,14 @@ class BatchedMPC:
             return dict(nominal=ms[0], riccati=ms[1], linearise=ms[2])
         return dict(nominal=ms[0], riccati=ms[1], forward=ms[2])
 
+    def last_kernels(self) -> dict:
+        """{phase: rocprof kernel name} of what the last solve launched (phases as ``last_timing``)."""
+        return _lib.kernel_names(lambda b, n: self.lib.mpcb_last_kernels(self._h, b, n), self.nx == 17)
+
+    def plan_kernels(self, B: int, iterate: bool = False, want_traj: bool = True) -> dict:
+        """{phase: rocprof kernel name} a solve of B instances launches on this handle's config."""
+        return _lib.plan_kernels(self._c, self.max_batch, B, iterate, want_traj)
+
     def _dev(self, t, shape_tail, name, batch=None, allow_broadcast=False):
         """Coerce to a contiguous device tensor of the handle dtype; return (tensor, stride)."""
         torch = _torch()

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_bo
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
-  if (a.as_queue) {   // as many waves as stay resident; the rest of the chunk comes off the counter
+  if (a.as_queue && !dry_run()) {   // as many waves as stay resident; the rest of the chunk comes off the counter
     static const unsigned resident = [] {
       int dev = 0, cus = 0;
       if (hipGetDevice(&dev) != hipSuccess ||
@@ -55,32 +55,32 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   const bool it = MPCB_AS_ITER_T && a.mode == MPCB_MODE_ITERATE;
   if constexpr (sizeof(T) == 4) {
     if (it) {
-      if (w32) hipLaunchKernelGGL((as_kernel_f32<true, true>), dim3(g), dim3(64), lds, st, a);
-      else hipLaunchKernelGGL((as_kernel_f32<false, true>), dim3(g), dim3(64), lds, st, a);
+      if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f32<true, true>), dim3(g), dim3(64), lds, st, a);
+      else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f32<false, true>), dim3(g), dim3(64), lds, st, a);
     } else {
-      if (w32) hipLaunchKernelGGL(as_kernel_f32<true>, dim3(g), dim3(64), lds, st, a);
-      else hipLaunchKernelGGL(as_kernel_f32<false>, dim3(g), dim3(64), lds, st, a);
+      if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f32<true>), dim3(g), dim3(64), lds, st, a);
+      else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f32<false>), dim3(g), dim3(64), lds, st, a);
     }
   } else {
     if (it) {
-      if (w32) hipLaunchKernelGGL((as_kernel_f64<true, true>), dim3(g), dim3(64), lds, st, a);
-      else hipLaunchKernelGGL((as_kernel_f64<false, true>), dim3(g), dim3(64), lds, st, a);
+      if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<true, true>), dim3(g), dim3(64), lds, st, a);
+      else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<false, true>), dim3(g), dim3(64), lds, st, a);
     } else {
-      if (w32) hipLaunchKernelGGL(as_kernel_f64<true>, dim3(g), dim3(64), lds, st, a);
-      else hipLaunchKernelGGL(as_kernel_f64<false>, dim3(g), dim3(64), lds, st, a);
+      if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<true>), dim3(g), dim3(64), lds, st, a);
+      else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<false>), dim3(g), dim3(64), lds, st, a);
     }
   }
-  return hipGetLastError();
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 // forward pass of the unconstrained small-chunk path from P2's row-major exports (ABT2, KR2)
 template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
   if (MPCB_AS_ITER_T && a.mode == MPCB_MODE_ITERATE)
-    hipLaunchKernelGGL((fwd_rm_kernel<T, true>), dim3(g), dim3(64), lds, st, a);
+    MPCB_LAUNCH(PH_FORWARD, (fwd_rm_kernel<T, true>), dim3(g), dim3(64), lds, st, a);
   else
-    hipLaunchKernelGGL(fwd_rm_kernel<T>, dim3(g), dim3(64), lds, st, a);
-  return hipGetLastError();
+    MPCB_LAUNCH(PH_FORWARD, (fwd_rm_kernel<T>), dim3(g), dim3(64), lds, st, a);
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 template hipError_t launch_fwd_rm<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_fwd_rm<float>(const SplitArgs<float>&, hipStream_t);
@@ -91,7 +91,7 @@ template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p3(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
 }
 extern "C" int mpcb_debug_stamps_as(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_astamps), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -2;

@@ -504,15 +504,6 @@ box_kernel_f32(SplitArgs<float> a) { box_body<float, MODE>(a); }
 template <int MODE>
 __global__ void __launch_bounds__(64) box_kernel_f64(SplitArgs<double> a) { box_body<double, MODE>(a); }
 
-template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st) {
-  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32<PASS_BOX>, dim3(g), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(box_kernel_f64<PASS_BOX>, dim3(g), dim3(64), 0, st, a);
-  return hipGetLastError();
-}
-
 // ---- small unconstrained batches -------------------------------------------------------------
 // The Riccati pass of the split path integrates 16 RK4 tangents per stage inside its serial
 // backward recursion; at a few thousand instances (c2: 4096, one wavefront per SIMD) that
@@ -555,30 +546,16 @@ __global__ void __launch_bounds__(64) lin_kernel(SplitArgs<T> a) {
 
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st) {
   const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  hipLaunchKernelGGL((lin_kernel<T>), dim3(g, a.N), dim3(64), 0, st, a);
+  MPCB_LAUNCH(PH_LIN, (lin_kernel<T>), dim3(g, a.N), dim3(64), 0, st, a);
   if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32<PASS_SMALL>, dim3(g), dim3(64), 0, st, a);
+    MPCB_LAUNCH(PH_RICCATI, (box_kernel_f32<PASS_SMALL>), dim3(g), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL(box_kernel_f64<PASS_SMALL>, dim3(g), dim3(64), 0, st, a);
-  return hipGetLastError();
+    MPCB_LAUNCH(PH_RICCATI, (box_kernel_f64<PASS_SMALL>), dim3(g), dim3(64), 0, st, a);
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 
-// forward pass of the plain split path in the 16-lane layout, from P2's gains and [A|B]^T
-template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st) {
-  const unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(box_kernel_f32<PASS_FWD>, dim3(g), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(box_kernel_f64<PASS_FWD>, dim3(g), dim3(64), 0, st, a);
-  return hipGetLastError();
-}
-
-template hipError_t launch_box<double>(const SplitArgs<double>&, hipStream_t);
-template hipError_t launch_box<float>(const SplitArgs<float>&, hipStream_t);
 template hipError_t launch_small<double>(const SplitArgs<double>&, hipStream_t);
 template hipError_t launch_small<float>(const SplitArgs<float>&, hipStream_t);
-template hipError_t launch_fwd16<double>(const SplitArgs<double>&, hipStream_t);
-template hipError_t launch_fwd16<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb
 

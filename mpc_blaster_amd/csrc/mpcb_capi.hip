@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <cstddef>
 #include <cstring>
+#include <cxxabi.h>
+#include <dlfcn.h>
 #include <string>
 
 #include "../../include/mpcb.h"
@@ -52,6 +54,13 @@ bool inv3(const double* A, double* out) {
 }
 }  // namespace
 
+namespace mpcb {
+LaunchLog& launch_log() {
+  thread_local LaunchLog g{};
+  return g;
+}
+}  // namespace mpcb
+
 struct mpcb_handle {
   mpcb_config cfg;
   int device;
@@ -85,6 +94,7 @@ struct mpcb_handle {
   int64_t params_count = 0;   // instance rows behind params (checked against B when params_sb != 0)
   int32_t* qp_stats = nullptr;   // 12/4 input box: per instance [forward passes, masked stages]
   int64_t qp_stats_rows = 0;     // instances of the last boxed solve
+  const void* last_fn[LOG_SLOTS] = {};   // kernels the last solve launched (mpcb_last_kernels)
 };
 
 // A 17/6 call over B instances may only read parameter rows that exist (mpcb_set_params count).
@@ -158,9 +168,7 @@ static void fill_model(const mpcb_config& c, const double* Jinv, Model<T>& M) {
   }
 }
 
-extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
-  if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");
-  *out = nullptr;
+static int validate_config(const mpcb_config* cfg, int64_t max_batch, double Jinv[9]) {
   const bool full = cfg->nx == NX17 && cfg->nu == NU17;
   if (!(cfg->nx == NX && cfg->nu == NU) && !full)
     return fail(MPCB_E_UNSUPPORTED, "nx=%d nu=%d: implemented models are 12/4 (rigid-body slice) and 17/6 (full)",
@@ -186,29 +194,31 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   if (!(cfg->dt > 0) || !(cfg->mass > 0)) return fail(MPCB_E_INVALID, "dt and mass must be > 0");
   if (max_batch < 1) return fail(MPCB_E_INVALID, "max_batch=%lld", (long long)max_batch);
   if (cfg->box_u && cfg->max_as_iter < 1) return fail(MPCB_E_INVALID, "max_as_iter must be >= 1");
-  double Jinv[9];
   if (!inv3(cfg->J, Jinv)) return fail(MPCB_E_INVALID, "inertia J is singular");
-  int ndev = 0;
-  HIP_TRY(hipGetDeviceCount(&ndev));
-  if (device < 0 || device >= ndev) return fail(MPCB_E_INVALID, "device %d of %d", device, ndev);
-  HIP_TRY(hipSetDevice(device));
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  return MPCB_OK;
+}
 
-  mpcb_handle* h = new mpcb_handle();
+// LDS of one workgroup at one wave per SIMD: 4 workgroups share a CU's 160 KiB
+constexpr size_t LDS_PER_WAVE_SIMD = 160 * 1024 / 4;
+// the dynamic LDS a workgroup may ask for without an attribute
+constexpr size_t LDS_DYN_MAX = 64 * 1024;
+
+// Kernel variants of a handle: a pure function of the config and max_batch (and MPCB_* switches
+// that tests exercise), shared by mpcb_create and the device-free mpcb_plan_kernels.
+static void select_path(mpcb_handle* h, const mpcb_config* cfg, int64_t max_batch, int cus) {
+  const bool full = cfg->nx == NX17 && cfg->nu == NU17;
   h->cfg = *cfg;
-  h->device = device;
   h->max_batch = max_batch;
   const bool f64 = cfg->dtype == MPCB_F64;
   // resident slots: one 64-thread workgroup per slot, a few per SIMD
   const int64_t waves_needed = (max_batch + GROUPS - 1) / GROUPS;
-  int64_t grid = (int64_t)prop.multiProcessorCount * 16;
+  int64_t grid = (int64_t)cus * 16;
   if (grid > waves_needed) grid = waves_needed;
   h->grid = (int)grid;
   const size_t esz = f64 ? sizeof(double) : sizeof(float);
   // Path: the split kernels win at every measured batch size (c2: 4096); the single-kernel
-  // solver (mpcb_solve.hip) serves the input-box active-set loop and, on request
-  // (MPCB_SPLIT_MIN_BATCH above the batch), small unconstrained batches.
+  // solver (mpcb_solve.hip) serves, on request, small unconstrained batches
+  // (MPCB_SPLIT_MIN_BATCH above the batch) and the first input-box design (MPCB_BOX_IMPL=v1).
   if (full) {
     // one chunk of instances per launch triple; ~N*516 scalars of workspace each
     int64_t chunk = 8192;
@@ -221,58 +231,80 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     // (+3 instances: a ragged last wavefront of the 16-lane kernel works in private padding slots)
     h->chunk_elems = full17_elems(cfg->N) * ((chunk + 3) / 4 * 4);
     h->scratch_bytes = h->chunk_elems * (int64_t)esz;
+    return;
   }
   int64_t split_min = 1;
   if (const char* e = getenv("MPCB_SPLIT_MIN_BATCH")) split_min = atoll(e);
-  if (!full) h->split = (max_batch >= split_min) ? 1 : 0;
+  h->split = (max_batch >= split_min) ? 1 : 0;
   if (const char* e = getenv("MPCB_BOX_IMPL"))   // "v1": the single-kernel active-set solver
     if (cfg->box_u && strcmp(e, "v1") == 0) h->split = 0;
-  if (full) {
-  } else if (!h->split) {
+  if (!h->split) {
     h->slot_elems = f64 ? solve_slot_elems<double>(cfg->N, cfg->box_u) : solve_slot_elems<float>(cfg->N, cfg->box_u);
     h->scratch_bytes = h->slot_elems * (int64_t)esz * grid;
-  } else {
-    // chunk of instances whose intermediates (~N*160 scalars each) stay near the 256 MiB
-    // Infinity Cache while still giving the Riccati kernel >= 4 wavefronts per SIMD
-    int64_t chunk = 65536;
-    if (const char* e = getenv("MPCB_CHUNK")) chunk = atoll(e);
-    if (chunk < 64) chunk = 64;
-    if (chunk > max_batch) chunk = max_batch;
-    h->chunk = chunk;
-    // optional (MPCB_SMALL_MAX): linearise all stages in parallel and run the Riccati recursion
-    // over the cached [A|B].  Measured slower at c2 (lin 62 + passes 172 us vs P2+P3 187 us):
-    // the recursion's latency is its LDS exchanges, not the tangents, so it is off by default.
-    int64_t small_max = 0;
-    if (const char* e = getenv("MPCB_SMALL_MAX")) small_max = atoll(e);
-    h->small = (!cfg->box_u && chunk <= small_max) ? 1 : 0;
-    // small chunks: the forward pass in the 16-lane layout from P2's exported [A|B]^T (the
-    // thread-per-instance pass is latency-bound at a few thousand instances)
-    int64_t fwd16_max = 16384;
-    if (const char* e = getenv("MPCB_FWD16_MAX")) fwd16_max = atoll(e);
-    h->fwd16 = (!cfg->box_u && !h->small && chunk <= fwd16_max) ? 1 : 0;
-    int64_t quad_max = 16384;   // the rollout with a lane quad per instance (latency-bound sizes)
-    if (const char* e = getenv("MPCB_QUAD_P1_MAX")) quad_max = atoll(e);
-    // the 16-lane row rollout (f split over the lanes, mpcb_rollout.hip) below MPCB_ROW_P1_MAX
-    int64_t row_max = 16384;
-    if (const char* e = getenv("MPCB_ROW_P1_MAX")) row_max = atoll(e);
-    // (the row rollout stages the wave's u / xbar records in LDS: N <= 120 keeps them <= 64 KiB)
-    h->quad_p1 = (chunk <= row_max && cfg->N <= 120) ? 2 : (chunk <= quad_max) ? 1 : 0;
-    // the row rollout also integrates the tangents and exports [A|B] (MPCB_P1_TAN: default on in
-    // fp64; in fp32 its regrouped tangent algebra doubled the worst U error of the N=60 box test,
-    // 3.7e-5 -> 7.3e-5 against the 5e-5 bound, so fp32 keeps the captured scalars); P2 then reads
-    // [A|B] instead of integrating it
-    h->tin = (h->quad_p1 == 2 && !h->small && f64) ? 1 : 0;
-    if (const char* e = getenv("MPCB_P1_TAN")) if (atoi(e) == 0) h->tin = 0;
-    // ... and P2 runs in the same launch (row_riccati_kernel) unless MPCB_FUSE_P12=0
-    if (h->tin)
-      if (const char* e = getenv("MPCB_FUSE_P12")) if (atoi(e) == 0) h->tin = 2;
-    const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
-    const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
-                            : split_elems_per_instance<float>(cfg->N, 1, ab);
-    // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
-    h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
-    h->scratch_bytes = h->chunk_elems * (int64_t)esz;
+    return;
   }
+  // chunk of instances whose intermediates (~N*160 scalars each) stay near the 256 MiB
+  // Infinity Cache while still giving the Riccati kernel >= 4 wavefronts per SIMD
+  int64_t chunk = 65536;
+  if (const char* e = getenv("MPCB_CHUNK")) chunk = atoll(e);
+  if (chunk < 64) chunk = 64;
+  if (chunk > max_batch) chunk = max_batch;
+  h->chunk = chunk;
+  // optional (MPCB_SMALL_MAX): linearise all stages in parallel and run the Riccati recursion
+  // over the cached [A|B].  Measured slower at c2 (lin 62 + passes 172 us vs P2+P3 187 us):
+  // the recursion's latency is its LDS exchanges, not the tangents, so it is off by default.
+  int64_t small_max = 0;
+  if (const char* e = getenv("MPCB_SMALL_MAX")) small_max = atoll(e);
+  h->small = (!cfg->box_u && chunk <= small_max) ? 1 : 0;
+  // chunks of at most 16384 instances (c2: 4096, one wave per SIMD, latency-bound) use the
+  // 16-lane kernels: the forward pass over P2's row-major exports and the row rollout (f split
+  // over the 16 lanes of an instance, mpcb_rollout.hip); larger chunks (c3, c5) run the
+  // thread-per-instance rollout and forward pass (the lane-quad rollout measured slower there:
+  // c3 P1 0.098 vs 0.090 ms, c5 0.38 vs 0.34 ms)
+  const bool lat = chunk <= 16384;
+  h->fwd16 = (!cfg->box_u && !h->small && lat) ? 1 : 0;
+  // the row rollout stages the wave's u / xbar records in dynamic LDS (mpcb_row.h row_lds_bytes,
+  // sized here for iterate mode, the larger carve); beyond 64 KiB the lane-quad rollout
+  const size_t row_lds = (size_t)GROUPS * ((size_t)cfg->N * NU + (size_t)(cfg->N + 1) * NX) * esz;
+  h->quad_p1 = lat ? (row_lds <= LDS_DYN_MAX ? 2 : 1) : 0;
+  // the row rollout also integrates the tangents and exports [A|B] (MPCB_P1_TAN: default on in
+  // fp64; in fp32 its regrouped tangent algebra doubled the worst U error of the N=60 box test,
+  // 3.7e-5 -> 7.3e-5 against the 5e-5 bound, so fp32 keeps the captured scalars); P2 then reads
+  // [A|B] instead of integrating it.  Only where a consumer of the row-major exports runs (the
+  // 16-lane forward pass or the active-set kernel): the thread-per-instance forward reads the CC
+  // record, which the tangent rollout does not write.
+  h->tin = (h->quad_p1 == 2 && !h->small && f64 && (cfg->box_u || h->fwd16)) ? 1 : 0;
+  if (const char* e = getenv("MPCB_P1_TAN")) if (atoi(e) == 0) h->tin = 0;
+  // ... and P2 runs in the same launch (row_riccati_kernel) when the two bodies' LDS still
+  // leaves one wave per SIMD resident, unless MPCB_FUSE_P12=0
+  if (h->tin && row_lds + RICCATI_F64_STATIC_LDS > LDS_PER_WAVE_SIMD) h->tin = 2;
+  if (h->tin)
+    if (const char* e = getenv("MPCB_FUSE_P12")) if (atoi(e) == 0) h->tin = 2;
+  const int ab = cfg->box_u ? 2 : ((h->small || h->fwd16 || h->tin) ? 1 : 0);
+  const int64_t per = f64 ? split_elems_per_instance<double>(cfg->N, 1, ab)
+                          : split_elems_per_instance<float>(cfg->N, 1, ab);
+  // (+64: the forward's row loads may read up to 4 elements past the last ABT2 row)
+  h->chunk_elems = per * ((chunk + 3) / 4 * 4) + 64;
+  h->scratch_bytes = h->chunk_elems * (int64_t)esz;
+}
+
+extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
+  if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");
+  *out = nullptr;
+  double Jinv[9];
+  if (int rc = validate_config(cfg, max_batch, Jinv)) return rc;
+  const bool full = cfg->nx == NX17 && cfg->nu == NU17;
+  const bool f64 = cfg->dtype == MPCB_F64;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MPCB_E_INVALID, "device %d of %d", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+
+  mpcb_handle* h = new mpcb_handle();
+  h->device = device;
+  select_path(h, cfg, max_batch, prop.multiProcessorCount);
   fill_model(*cfg, Jinv, h->Md);
   fill_model(*cfg, Jinv, h->Mf);
   hipError_t e = hipMalloc(&h->scratch, (size_t)h->scratch_bytes);
@@ -353,7 +385,7 @@ extern "C" int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* stre
 }
 
 template <class T>
-static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64_t x0_sb,
+static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64_t x0_sb,
                       const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
                       const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
                       void* u0, void* X, void* U, int32_t* status, void* stream) {
@@ -428,7 +460,6 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
       a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
       a.imajor = h->cfg.box_u ? 0 : 1;
-      if (const char* e = getenv("MPCB_RM_IMAJOR")) a.imajor = atoi(e) != 0;
       a.AB = ((h->cfg.box_u && MPCB_AS_AB2) || h->small) ? ab : nullptr;
       a.ABT = (h->cfg.box_u || h->small || h->tin || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
@@ -478,6 +509,82 @@ static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     h->timed_split = 0;
   }
   return MPCB_OK;
+}
+
+// solve_body with the launch log: the kernels this solve launches (or, in a dry run, would launch)
+template <class T>
+static int solve_impl(mpcb_handle* h, int64_t B, int mode, const void* x0, int64_t x0_sb,
+                      const void* xbar, const void* ubar, const void* xref, int64_t xref_sb,
+                      const void* uref, int64_t uref_sb, const void* wind, int64_t wind_sb,
+                      void* u0, void* X, void* U, int32_t* status, void* stream) {
+  LaunchLog& L = launch_log();
+  for (auto& f : L.fn) f = nullptr;
+  const int rc = solve_body<T>(h, B, mode, x0, x0_sb, xbar, ubar, xref, xref_sb, uref, uref_sb, wind,
+                               wind_sb, u0, X, U, status, stream);
+  for (int i = 0; i < LOG_SLOTS; ++i) h->last_fn[i] = L.fn[i];
+  return rc;
+}
+
+// "mpcb::riccati_kernel_f32<false, false, false>": the demangled kernel symbol without its return
+// type and parameters, as rocprofv3 names the dispatch (a kernel's host handle is a dynamic symbol
+// of this library named like the device function)
+static std::string kernel_name(const void* fn) {
+  if (!fn) return "";
+  Dl_info inf;
+  if (!dladdr(fn, &inf) || !inf.dli_sname) return "?";
+  int st = 0;
+  char* d = abi::__cxa_demangle(inf.dli_sname, nullptr, nullptr, &st);
+  std::string s = d ? d : inf.dli_sname;
+  free(d);
+  if (s.rfind("void ", 0) == 0) s = s.substr(5);
+  int depth = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '<') ++depth;
+    else if (s[i] == '>') --depth;
+    else if (s[i] == '(' && depth == 0) return s.substr(0, i);
+  }
+  return s;
+}
+
+static int write_kernel_names(const void* const fn[LOG_SLOTS], char* buf, int64_t len) {
+  std::string out;
+  for (int i = 0; i < LOG_SLOTS; ++i) out += kernel_name(fn[i]) + (i + 1 < LOG_SLOTS ? "\n" : "");
+  if (!buf || len < (int64_t)out.size() + 1)
+    return fail(MPCB_E_INVALID, "kernel names need a buffer of %zu bytes", out.size() + 1);
+  memcpy(buf, out.c_str(), out.size() + 1);
+  return MPCB_OK;
+}
+
+extern "C" int mpcb_plan_kernels(const mpcb_config* cfg, int64_t max_batch, int64_t B, int mode, int want_traj,
+                                 char* buf, int64_t len) {
+  if (!cfg) return fail(MPCB_E_INVALID, "null config");
+  double Jinv[9];
+  if (int rc = validate_config(cfg, max_batch, Jinv)) return rc;
+  if (B < 1 || B > max_batch) return fail(MPCB_E_INVALID, "batch %lld outside 1..max_batch", (long long)B);
+  if (mode != MPCB_MODE_ROLLOUT && mode != MPCB_MODE_ITERATE) return fail(MPCB_E_INVALID, "mode=%d", mode);
+  mpcb_handle h;
+  h.device = -1;
+  select_path(&h, cfg, max_batch, 256);
+  fill_model(*cfg, Jinv, h.Md);
+  fill_model(*cfg, Jinv, h.Mf);
+  // (never dereferenced: a dry run makes no HIP call and launches nothing)
+  alignas(16) static double dummy[64];
+  void* d = dummy;
+  LaunchLog& L = launch_log();
+  L.dry = true;
+  int rc = cfg->dtype == MPCB_F64
+               ? solve_impl<double>(&h, B, mode, d, 0, d, d, d, 0, d, 0, nullptr, 0, d, want_traj ? d : nullptr,
+                                    want_traj ? d : nullptr, (int32_t*)d, nullptr)
+               : solve_impl<float>(&h, B, mode, d, 0, d, d, d, 0, d, 0, nullptr, 0, d, want_traj ? d : nullptr,
+                                   want_traj ? d : nullptr, (int32_t*)d, nullptr);
+  L.dry = false;
+  if (rc) return rc;
+  return write_kernel_names(h.last_fn, buf, len);
+}
+
+extern "C" int mpcb_last_kernels(const mpcb_handle* h, char* buf, int64_t len) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  return write_kernel_names(h->last_fn, buf, len);
 }
 
 extern "C" int mpcb_set_timing(mpcb_handle* h, int enable) {

@@ -36,18 +36,22 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 // table, s_memrealtime (100 MHz, one clock for the whole chip) at slot 0 entry, 1 loop start,
 // 2 loop end, 3 exit; lane 0 of each of the first 4096 workgroups writes it (a vector store).
 #ifdef MPCB_STAMPS
-#define WT_TABLE(name) __device__ unsigned long long name[4096 * 5];
-// slot 4 of the table (entries 4096 * 4 + wg): the wave's HW_ID (SIMD, CU, SE) and XCC_ID
+// waves recorded per kernel (c3 / c5 P2: 16384 / 32768 one-wave workgroups)
+#ifndef MPCB_WT_MAX
+#define MPCB_WT_MAX 32768
+#endif
+#define WT_TABLE(name) __device__ unsigned long long name[MPCB_WT_MAX * 5];
+// slot 4 of the table (entries MPCB_WT_MAX * 4 + wg): the wave's HW_ID (SIMD, CU, SE) and XCC_ID
 #define WT_HW(name)                                                                 \
   {                                                                                 \
     const unsigned hw_ = __builtin_amdgcn_s_getreg(63492), xcc_ = __builtin_amdgcn_s_getreg(63508); \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                               \
-      name[4096 * 4 + blockIdx.x] = ((unsigned long long)xcc_ << 32) | hw_;        \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < MPCB_WT_MAX)                        \
+      name[MPCB_WT_MAX * 4 + blockIdx.x] = ((unsigned long long)xcc_ << 32) | hw_; \
   }
 #define WT(name, slot)                                                              \
   {                                                                                 \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) name[blockIdx.x * 4 + (slot)] = t_; \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < MPCB_WT_MAX) name[blockIdx.x * 4 + (slot)] = t_; \
   }
 #else
 #define WT_TABLE(name)

@@ -245,14 +245,14 @@ __global__ void __launch_bounds__(64) sim17_kernel(int64_t B, T h, Model<T> M, c
 
 template <class T> hipError_t launch_full17(const FullArgs<T>& a, hipStream_t st, hipEvent_t* ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(nominal17q_kernel<T>, dim3((unsigned)((a.nb + 3) / 4)), dim3(64), 0, st, a);
+  MPCB_LAUNCH(PH_NOMINAL, (nominal17q_kernel<T>), dim3((unsigned)((a.nb + 3) / 4)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(lin17ws_kernel<T>, dim3((unsigned)((a.nb * a.N + GQ17 - 1) / GQ17)), dim3(64), 0, st, a);
+  MPCB_LAUNCH(PH_LIN17, (lin17ws_kernel<T>), dim3((unsigned)((a.nb * a.N + GQ17 - 1) / GQ17)), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
   const hipError_t e = launch_riccati17q<T>(a, st);
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[3], st);
-  return hipGetLastError();
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 template <class T>
 hipError_t launch_linearize17(int64_t B, int N, T h, const Model<T>& M, const T* p, int64_t p_sb,

@@ -54,6 +54,31 @@ struct SolveArgs {
 
 template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipStream_t st);
 
+// Launch log of the solve paths (mpcb_plan_kernels / mpcb_last_kernels, include/mpcb.h): every
+// solve-path launcher notes the kernel it launches in the slot of its timing phase
+// (mpcb_last_timing: 0 nominal, 1 Riccati / the single launch, 2 forward pass or the 17/6
+// stage-parallel linearisation; 3 the small-chunk path's linearisation).  In a dry run (the plan
+// of a config, no device) the launchers note their kernels and make no HIP call, so the plan and
+// the launches come from the same selection code.
+constexpr int LOG_SLOTS = 4;
+struct LaunchLog {
+  const void* fn[LOG_SLOTS];
+  bool dry;
+};
+LaunchLog& launch_log();   // thread-local (mpcb_capi.hip)
+inline bool dry_run() { return launch_log().dry; }
+#define MPCB_LAUNCH(PH, K, G, BLK, LDS, ST, ...)                                \
+  do {                                                                          \
+    ::mpcb::launch_log().fn[PH] = reinterpret_cast<const void*>(&K);            \
+    if (!::mpcb::launch_log().dry) hipLaunchKernelGGL(K, G, BLK, LDS, ST, __VA_ARGS__); \
+  } while (0)
+enum { PH_NOMINAL = 0, PH_RICCATI = 1, PH_FORWARD = 2, PH_LIN17 = 2, PH_LIN = 3 };
+// Static LDS of the fp64 Riccati body (riccati_body: GroupLds x 4, SW, Cst), the same in
+// row_riccati_kernel and riccati_kernel_f64 (tools/kernel_meta.py: 24064 B); mpcb_create sizes
+// the fused launch with it and launch_split checks it against the code object before the first
+// fused launch (the solve fails loudly if it grew).
+constexpr size_t RICCATI_F64_STATIC_LDS = 24064;
+
 // Split (unconstrained) path: three launches per chunk of instances.
 //   P1 nominal  (thread / instance): rollout or iterate, captures linearisation scalars
 //   P2 riccati  (16 lanes / instance): tangent columns of [A|B] + Riccati, writes gains
@@ -142,11 +167,9 @@ struct SplitArgs {
 // ev (nullable): 4 events recorded on st before P1, after P1, after P2 and after P3.
 template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st,
                                            hipEvent_t* ev = nullptr);
-template <class T> hipError_t launch_box(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_fwd_rm(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_small(const SplitArgs<T>& a, hipStream_t st);
-template <class T> hipError_t launch_fwd16(const SplitArgs<T>& a, hipStream_t st);
 template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStream_t st);   // mpcb_rollout.hip
 template <class T> int64_t split_elems_per_instance(int N, int iterate, int box = 0);  // per instance
 template <class T> int64_t solve_slot_elems(int N, int box);

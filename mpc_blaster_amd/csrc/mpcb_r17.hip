@@ -1362,12 +1362,12 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
 template <class T> hipError_t launch_riccati17q(const FullArgs<T>& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.nb + q17::GR - 1) / q17::GR));
   if (a.box && !a.sbox && sizeof(T) == 8)
-    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true, true>), grid, dim3(64), 0, st, a);
+    MPCB_LAUNCH(PH_RICCATI, (q17::riccati17q_kernel<T, true, true>), grid, dim3(64), 0, st, a);
   else if (a.box)
-    hipLaunchKernelGGL((q17::riccati17q_kernel<T, true, false>), grid, dim3(64), 0, st, a);
+    MPCB_LAUNCH(PH_RICCATI, (q17::riccati17q_kernel<T, true, false>), grid, dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL((q17::riccati17q_kernel<T, false, false>), grid, dim3(64), 0, st, a);
-  return hipGetLastError();
+    MPCB_LAUNCH(PH_RICCATI, (q17::riccati17q_kernel<T, false, false>), grid, dim3(64), 0, st, a);
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 template hipError_t launch_riccati17q<double>(const FullArgs<double>&, hipStream_t);
 template hipError_t launch_riccati17q<float>(const FullArgs<float>&, hipStream_t);

@@ -22,11 +22,11 @@ static void launch_row_m(const SplitArgs<T>& a, hipStream_t st) {
   const bool dj = row_dj(a);
   const bool it = a.mode == MPCB_MODE_ITERATE;
   if (dj) {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, true, TAN>), grid, dim3(64), lds, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, true, TAN>), grid, dim3(64), lds, st, a);
+    if (it) MPCB_LAUNCH(PH_NOMINAL, (nominal_row_kernel<T, true, true, TAN>), grid, dim3(64), lds, st, a);
+    else MPCB_LAUNCH(PH_NOMINAL, (nominal_row_kernel<T, false, true, TAN>), grid, dim3(64), lds, st, a);
   } else {
-    if (it) hipLaunchKernelGGL((nominal_row_kernel<T, true, false, TAN>), grid, dim3(64), lds, st, a);
-    else hipLaunchKernelGGL((nominal_row_kernel<T, false, false, TAN>), grid, dim3(64), lds, st, a);
+    if (it) MPCB_LAUNCH(PH_NOMINAL, (nominal_row_kernel<T, true, false, TAN>), grid, dim3(64), lds, st, a);
+    else MPCB_LAUNCH(PH_NOMINAL, (nominal_row_kernel<T, false, false, TAN>), grid, dim3(64), lds, st, a);
   }
 }
 
@@ -34,13 +34,13 @@ template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStrea
   // (the tangent export is built for fp64 only: mpcb_create sets tin there)
   if (sizeof(T) == 8 && a.tin) launch_row_m<T, sizeof(T) == 8>(a, st);
   else launch_row_m<T, false>(a, st);
-  return hipGetLastError();
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 
 template hipError_t launch_nominal_row<double>(const SplitArgs<double>&, hipStream_t);
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p1(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
 }
 #endif
 template hipError_t launch_nominal_row<float>(const SplitArgs<float>&, hipStream_t);

@@ -432,10 +432,10 @@ template <class T> int64_t solve_slot_elems(int N, int box) {
 
 template <class T> hipError_t launch_solve(const SolveArgs<T>& a, int grid, hipStream_t st) {
   if (a.box)
-    hipLaunchKernelGGL((solve_kernel<T, 1>), dim3(grid), dim3(64), 0, st, a);
+    MPCB_LAUNCH(PH_RICCATI, (solve_kernel<T, 1>), dim3(grid), dim3(64), 0, st, a);
   else
-    hipLaunchKernelGGL((solve_kernel<T, 0>), dim3(grid), dim3(64), 0, st, a);
-  return hipGetLastError();
+    MPCB_LAUNCH(PH_RICCATI, (solve_kernel<T, 0>), dim3(grid), dim3(64), 0, st, a);
+  return dry_run() ? hipSuccess : hipGetLastError();
 }
 
 template hipError_t launch_solve<double>(const SolveArgs<double>&, int, hipStream_t);

@@ -1119,33 +1119,17 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_kernel(SplitArgs
   riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
-// ... and the forward pass of the quad too (MPCB_FUSE_FWD=1): the waves that finish their
-// Riccati recursion early stream their forward pass while the slow ones still factorise.
-// Measured at c2: 0.0986-0.1003 vs 0.1003-0.1007 ms with fwd_rm as its own launch, within the
-// run-to-run spread, so off (fwd_rm keeps its own launch and roofline line)
-#ifndef MPCB_FUSE_FWD
-#define MPCB_FUSE_FWD 0
-#endif
-template <bool ITER, bool DJ>
-__global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_fwd_kernel(SplitArgs<double> a) {
-  row_body<double, ITER, DJ, true>(a);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  asq::as_body<double, false, false, ITER>(a);
-}
-
 template <class T, bool USE_CC, bool ITER>
 static hipError_t launch_forward_m(const SplitArgs<T>& a, unsigned grid, hipStream_t st) {
   constexpr size_t bytes = FwdLds<T, USE_CC>::BYTES;
   static_assert(bytes <= 160 * 1024, "P3 LDS carve exceeds the CU's 160 KiB");
-  static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&forward_kernel<T, USE_CC, ITER>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((forward_kernel<T, USE_CC, ITER>), dim3(grid), dim3(WAVE), bytes, st, a);
+  if (!dry_run()) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&forward_kernel<T, USE_CC, ITER>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (attr != hipSuccess) return attr;
+  }
+  MPCB_LAUNCH(PH_FORWARD, (forward_kernel<T, USE_CC, ITER>), dim3(grid), dim3(WAVE), bytes, st, a);
   return hipSuccess;
 }
 template <class T, bool USE_CC>
@@ -1159,32 +1143,28 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
   const unsigned g64 = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
   if (ev) (void)hipEventRecord(ev[0], st);
   const bool fuse = sizeof(T) == 8 && MPCB_FUSE_P12 && a.quad_p1 == 2 && a.tin == 1 && !a.small;
-  const bool fuse3 = fuse && MPCB_FUSE_FWD && a.fwd && a.fwd16 && !a.GH;
   if (fuse) {
     // (the phase events: "nominal" empty, "riccati" the fused kernel)
     if (ev) (void)hipEventRecord(ev[1], st);
     const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
-    size_t lds = row_lds_bytes(a);
+    const size_t lds = row_lds_bytes(a);
     const bool it = a.mode == MPCB_MODE_ITERATE;   // (the row body's mode is always a template argument)
     if constexpr (sizeof(T) == 8) {
-      if (fuse3) {
-        const size_t lo = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
-        lds = lds > lo ? lds : lo;   // (the two bodies' dynamic LDS alias: one after the other)
-        const bool it3 = MPCB_AS_ITER_T && it;
-        if (!it3 && it) return hipErrorInvalidValue;   // (built with the mode as a template argument)
-        if (row_dj(a)) {
-          if (it3) hipLaunchKernelGGL((row_riccati_fwd_kernel<true, true>), grid, dim3(64), lds, st, a);
-          else hipLaunchKernelGGL((row_riccati_fwd_kernel<false, true>), grid, dim3(64), lds, st, a);
-        } else {
-          if (it3) hipLaunchKernelGGL((row_riccati_fwd_kernel<true, false>), grid, dim3(64), lds, st, a);
-          else hipLaunchKernelGGL((row_riccati_fwd_kernel<false, false>), grid, dim3(64), lds, st, a);
-        }
-      } else if (row_dj(a)) {
-        if (it) hipLaunchKernelGGL((row_riccati_kernel<true, true>), grid, dim3(64), lds, st, a);
-        else hipLaunchKernelGGL((row_riccati_kernel<false, true>), grid, dim3(64), lds, st, a);
+      if (!dry_run()) {
+        static const hipError_t lds_ok = [] {
+          hipFuncAttributes at;
+          hipError_t e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&row_riccati_kernel<false, true>));
+          if (e == hipSuccess && at.sharedSizeBytes > RICCATI_F64_STATIC_LDS) e = hipErrorInvalidConfiguration;
+          return e;
+        }();
+        if (lds_ok != hipSuccess) return lds_ok;
+      }
+      if (row_dj(a)) {
+        if (it) MPCB_LAUNCH(PH_RICCATI, (row_riccati_kernel<true, true>), grid, dim3(64), lds, st, a);
+        else MPCB_LAUNCH(PH_RICCATI, (row_riccati_kernel<false, true>), grid, dim3(64), lds, st, a);
       } else {
-        if (it) hipLaunchKernelGGL((row_riccati_kernel<true, false>), grid, dim3(64), lds, st, a);
-        else hipLaunchKernelGGL((row_riccati_kernel<false, false>), grid, dim3(64), lds, st, a);
+        if (it) MPCB_LAUNCH(PH_RICCATI, (row_riccati_kernel<true, false>), grid, dim3(64), lds, st, a);
+        else MPCB_LAUNCH(PH_RICCATI, (row_riccati_kernel<false, false>), grid, dim3(64), lds, st, a);
       }
     }
   } else if (a.quad_p1 == 2) {
@@ -1192,28 +1172,28 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     if (e != hipSuccess) return e;
   } else if (a.quad_p1) {
     const dim3 gq((unsigned)((a.nb + QI - 1) / QI));
-    if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((nominal_quad_kernel<T, true>), gq, dim3(WAVE), 0, st, a);
-    else hipLaunchKernelGGL((nominal_quad_kernel<T, false>), gq, dim3(WAVE), 0, st, a);
+    if (a.mode == MPCB_MODE_ITERATE) MPCB_LAUNCH(PH_NOMINAL, (nominal_quad_kernel<T, true>), gq, dim3(WAVE), 0, st, a);
+    else MPCB_LAUNCH(PH_NOMINAL, (nominal_quad_kernel<T, false>), gq, dim3(WAVE), 0, st, a);
   }
   else if (a.mode == MPCB_MODE_ITERATE)
-    hipLaunchKernelGGL((nominal_kernel<T, true>), dim3(gw), dim3(WAVE), 0, st, a);
+    MPCB_LAUNCH(PH_NOMINAL, (nominal_kernel<T, true>), dim3(gw), dim3(WAVE), 0, st, a);
   else
-    hipLaunchKernelGGL((nominal_kernel<T, false>), dim3(gw), dim3(WAVE), 0, st, a);
+    MPCB_LAUNCH(PH_NOMINAL, (nominal_kernel<T, false>), dim3(gw), dim3(WAVE), 0, st, a);
   if (ev && !fuse) (void)hipEventRecord(ev[1], st);
   if (a.small) {   // linearisation + Riccati + forward over the cached [A|B] (mpcb_box.hip)
     hipError_t e = launch_small<T>(a, st);
     if (ev) (void)hipEventRecord(ev[2], st);
     if (ev) (void)hipEventRecord(ev[3], st);
-    return e != hipSuccess ? e : hipGetLastError();
+    return e != hipSuccess ? e : (dry_run() ? hipSuccess : hipGetLastError());
   }
   const bool it = MPCB_P2_ITER_T && a.mode == MPCB_MODE_ITERATE;
   if constexpr (sizeof(T) == 4) {
     if (it) {
-      if (a.ABT) hipLaunchKernelGGL((riccati_kernel_f32<true, true>), dim3(g64), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((riccati_kernel_f32<false, true>), dim3(g64), dim3(64), 0, st, a);
+      if (a.ABT) MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f32<true, true>), dim3(g64), dim3(64), 0, st, a);
+      else MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f32<false, true>), dim3(g64), dim3(64), 0, st, a);
     } else {
-      if (a.ABT) hipLaunchKernelGGL(riccati_kernel_f32<true>, dim3(g64), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL(riccati_kernel_f32<false>, dim3(g64), dim3(64), 0, st, a);
+      if (a.ABT) MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f32<true>), dim3(g64), dim3(64), 0, st, a);
+      else MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f32<false>), dim3(g64), dim3(64), 0, st, a);
     }
   } else {
     // one fp64 instantiation per mode (export guarded at run time): measured leaner than the
@@ -1221,29 +1201,26 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     if (fuse) {
       // (P2 ran in row_riccati_kernel)
     } else if (a.tin) {
-      if (it) hipLaunchKernelGGL((riccati_kernel_f64<true, true, true>), dim3(g64), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((riccati_kernel_f64<true, false, true>), dim3(g64), dim3(64), 0, st, a);
+      if (it) MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f64<true, true, true>), dim3(g64), dim3(64), 0, st, a);
+      else MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f64<true, false, true>), dim3(g64), dim3(64), 0, st, a);
     } else if (it) {
-      hipLaunchKernelGGL((riccati_kernel_f64<true, true>), dim3(g64), dim3(64), 0, st, a);
+      MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f64<true, true>), dim3(g64), dim3(64), 0, st, a);
     } else {
-      hipLaunchKernelGGL(riccati_kernel_f64<true>, dim3(g64), dim3(64), 0, st, a);
+      MPCB_LAUNCH(PH_RICCATI, (riccati_kernel_f64<true>), dim3(g64), dim3(64), 0, st, a);
     }
   }
   if (ev) (void)hipEventRecord(ev[2], st);
-  // Small chunks keep the captured scalars cache-resident: integrate the forward tangent from
-  // them (no sin/cos).  Large chunks re-evaluate f instead of streaming 80 scalars per stage
-  // back from HBM.
   hipError_t e = hipSuccess;
-  if (fuse3) {
-    // (the forward pass ran in row_riccati_fwd_kernel)
-  } else if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_as.hip)
+  if (a.GH)   // input boxes: active-set iterations over the exported linearisation (mpcb_as.hip)
     e = launch_as<T>(a, st);
   else if (a.fwd && a.fwd16)   // forward pass from the exported [A|B]^T, 16 lanes per instance
     e = launch_fwd_rm<T>(a, st);
-  else if (a.fwd)
-    e = (a.nb <= 16384) ? launch_forward<T, true>(a, gw, st) : launch_forward<T, false>(a, gw, st);
+  else if (a.fwd)   // (chunks above 16384: re-evaluates f rather than streaming 80 captured
+                    // scalars per stage back from HBM; the variant depends on the handle, not on
+                    // this call's batch, so an instance's outputs do not depend on its batch)
+    e = launch_forward<T, false>(a, gw, st);
   if (ev) (void)hipEventRecord(ev[3], st);
-  return e != hipSuccess ? e : hipGetLastError();
+  return e != hipSuccess ? e : (dry_run() ? hipSuccess : hipGetLastError());
 }
 
 template hipError_t launch_split<double>(const SplitArgs<double>&, hipStream_t, hipEvent_t*);
@@ -1257,12 +1234,13 @@ template int64_t split_elems_per_instance<float>(int, int, int);
 // (same translation unit as g_stamps: the library is built without -fgpu-rdc)
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p1f(unsigned long long* out) {   // the row body inside row_riccati_kernel
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
 }
 extern "C" int mpcb_debug_wt_p2(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * 4096 * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
 }
 #endif
+extern "C" int mpcb_debug_wt_max(void) { return MPCB_WT_MAX; }
 extern "C" int mpcb_debug_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
 }

@@ -62,6 +62,9 @@ class _StubSolver:
     def last_timing(self):
         return dict(nominal=0.01, riccati=0.02, forward=0.01)
 
+    def last_kernels(self):
+        return dict(nominal='stub::nominal', riccati='stub::riccati', forward='stub::forward')
+
     def qp_stats(self, B):
         return torch.from_numpy(self.stats[:B].copy())
 

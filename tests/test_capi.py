@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.EXPORTS) == set(declared)
-    assert lib.mpcb_abi_version() == 4
+    assert lib.mpcb_abi_version() == 5
 
 
 def test_config_struct_layout_matches_header():

@@ -62,7 +62,7 @@ def test_library_is_the_native_hip_build():
     from mpc_blaster_amd import _lib
     lib = _lib.load()
     assert os.path.basename(lib._name) == 'libmpcblaster.so'
-    assert lib.mpcb_abi_version() == 4
+    assert lib.mpcb_abi_version() == 5
 
 
 def test_linearize_matches_oracle_fp64():
@@ -268,6 +268,43 @@ def test_full_size_c3_properties():
     o = mpc_solve(x0, xr, np.full((len(idx), N, 4), np.float32(22.0725), dtype=np.float64), _spec(N))
     assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 5e-5
     assert relerr(X[idx].cpu().numpy(), o['X']).max() < 5e-5
+
+
+@pytest.mark.parametrize('B', [4096, 20000])
+def test_full_size_c2_properties(B):
+    """BASELINE c2 at the bench's size (4096 per GPU, fp64, N = 20, hover) on the default path the
+    bench times (the fused rollout + Riccati launch and the 16-lane forward pass), and the same
+    workload above the 16384-instance small-chunk threshold (the thread-per-instance rollout and
+    forward pass, captured-scalar P2): every status 0, shard invariance (a slice solved alone gives
+    identical bits), and sampled parity against the fp64 oracle at 1e-9."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    N = 20
+    m = BatchedMPC(MPCConfig(N=N, dtype='f64'), max_batch=B)
+    d = m.gen_inputs(B, seed=1002, ref='hover')
+    u0 = m.solve(d['x0'], d['xref'], d['uref'], want_traj=True).clone()
+    X = m.get_state_trajectory().clone()
+    U = m.get_input_trajectory().clone()
+    st = m.get_status().clone()
+    torch.cuda.synchronize()
+    k = m.last_kernels()
+    assert k == m.plan_kernels(B)
+    if B <= 16384:
+        assert k == {'riccati': 'mpcb::row_riccati_kernel<false, true>', 'forward': 'mpcb::fwd_rm_kernel<double, false>'}
+    else:
+        assert k['nominal'] == 'mpcb::nominal_kernel<double, false>'
+        assert k['forward'] == 'mpcb::forward_kernel<double, false, false>'
+    assert int((st != 0).sum()) == 0
+    assert torch.isfinite(u0).all() and torch.isfinite(X).all() and torch.isfinite(U).all()
+    sl = slice(B // 3, B // 3 + 203)   # a ragged slice, off the quad boundary
+    u_sub = m.solve(d['x0'][sl], d['xref'], d['uref'], want_traj=True).clone()
+    X_sub = m.get_state_trajectory().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(u_sub, u0[sl]) and torch.equal(X_sub, X[sl])
+    idx = np.unique(np.r_[np.arange(0, B, 61), B - 1])
+    o = mpc_solve(d['x0'][idx].cpu().numpy(), d['xref'].cpu().numpy(), d['uref'].cpu().numpy(), _spec(N))
+    assert relerr(u0[idx].cpu().numpy(), o['u0']).max() < 1e-9
+    assert relerr(X[idx].cpu().numpy(), o['X']).max() < 1e-9
+    assert relerr(U[idx].cpu().numpy(), o['U']).max() < 1e-9
 
 
 @pytest.mark.parametrize('want_traj', [False, True])

@@ -1,9 +1,9 @@
 set -e
+O=gpurun_out/r05_base; mkdir -p $O
 export TMPDIR=/tmp
-O=gpurun_out/last; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { grep -E "FAIL|Error|error|assert" $O/gpu_tests.log | tail -30; exit 1; }
-tail -1 $O/gpu_tests.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
-tail -1 $O/smoke.log
+timeout -k 10 60 ./tools/micro/mfma64_check > $O/mfma64_check.txt 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1
-tail -c 300 $O/bench_default.log
+timeout -k 10 300 python bench.py --workload c4 --cpu-budget 4 > $O/bench_c4.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_c4 -o run -- python3 bench.py --workload c4 --steps 20 --warmup 3 --no-cpu-baseline --no-latency > $O/stats_c4.log 2>&1
+echo base_done
