@@ -239,9 +239,10 @@ def run(w, world, rank, dev, steps, warmup, stub=None, dump_gather=None):
         if plan != kernels:
             raise SystemExit(f'launched kernels {kernels} differ from the plan {plan}')
     path = ' + '.join(kernels[k] for k in ('nominal', 'riccati', 'linearise', 'forward') if k in kernels)
+    split = mpc.path == 'split'
     mpc.close()
     return dict(elapsed=elapsed, kern_ms=kern_ms, bad=bad, path=path, phase_ms=phase_ms,
-                kernels=kernels, split=mpc.path == 'split', qp=qp, cuda=cuda)
+                kernels=kernels, split=split, qp=qp, cuda=cuda)
 
 
 def phase_kernels(w):

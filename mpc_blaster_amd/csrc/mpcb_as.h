@@ -163,9 +163,28 @@ template <bool W32> struct Masks {
 #ifdef MPCB_AS_STAMPS
 WT_TABLE(g_wt_p3)
 #endif
+// p as an opaque VGPR value that still addresses global memory (the address-space cast keeps the
+// loads and stores global_*: through a plain opaque pointer the compiler falls back to flat_*
+// accesses, which also count against lgkmcnt)
+template <class P> __device__ __forceinline__ P* vglobal(P* p) {
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+v"(v));
+  return (P*)(__attribute__((address_space(1))) P*)v;
+}
+
 template <class T, bool BOX, bool W32 = false, bool ITER = false>
-__device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
+__device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   if constexpr (!BOX) AS_WT(0);
+  // box kernel: the workspace and I/O pointers as opaque loop-invariant VGPRs (as P2's model
+  // constants): kept in scalar registers they were spilled to VGPR lanes and read back with
+  // v_readlane at every pass and instance change
+  SplitArgs<T> a = args;
+  if constexpr (BOX) {
+    a.XU = vglobal(a.XU); a.GP = vglobal(a.GP); a.ABT = vglobal(a.ABT); a.GH = vglobal(a.GH);
+    a.KR = vglobal(a.KR); a.PS = vglobal(a.PS); a.xref = vglobal(a.xref); a.uref = vglobal(a.uref);
+    a.u0 = vglobal(a.u0); a.X = vglobal(a.X); a.U = vglobal(a.U); a.status = vglobal(a.status);
+    a.qp_stats = vglobal(a.qp_stats); a.x0 = vglobal(a.x0);
+  }
   using Mk = Masks<W32>;
   using M = typename Mk::M;
   constexpr int WB = Mk::WB;
@@ -179,6 +198,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   const bool stl = j < NX;                          // state lane (else input lane ju)
   const uint64_t mst = lane_mask(stl);
   T* const PX = lds_px[q];
+  // the group's LDS slot of P's entry (i, jx): max(i, jx) * 12 + min(i, jx)
+  int sym[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) sym[i] = (i > jx ? i : jx) * NX + (i > jx ? jx : i);
   const int64_t nb = a.nb;
   const int N = a.N;
   // the RK4 tangent's position entry of a velocity column, h/6 * (1 + 2 + 2 + 1) as the tangent
@@ -198,7 +221,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   bool valid;
   int64_t c, b;
   const T *xr, *ur, *xrN;
-  Arr<T> XU, GP, AB, ABT, GH, KR, PS;
+  Arr<T> XU, GP, ABT, GH, KR, PS;
+  const T* cbase;
+  int64_t cstride;
+  const T* refp;
+  const int64_t refs = stl ? NX : NU;
+  const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
+  // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
+  const int cslot = j < 3 ? j : j - 3;
   auto bind = [&](int64_t c_raw) {
     valid = c_raw < nb;
     c = valid ? c_raw : nb - 1;       // an empty group shadows the last instance
@@ -208,20 +238,21 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
     xrN = xr + (int64_t)N * NX;
     XU = arr(a.XU, XU_REC, nq, c);
     GP = arr(iterate ? a.GP : (T*)nullptr, GP_REC, nq, c);
-    AB = arr2(BOX ? a.AB : (T*)nullptr, AB2_REC, nq, c, N, a.imajor);
     ABT = arr2(a.ABT, ABT2_REC, nq, c, N, a.imajor);
     GH = arr2(BOX ? a.GH : (T*)nullptr, GH2_REC, nq, c, N, a.imajor);
     KR = arr2(a.KR, KR2_REC, nq, c, N, a.imajor);
     PS = arr2(BOX ? a.PS : (T*)nullptr, PS2_REC, nq, c, N, a.imajor);
+    // the masked backward's column loads: ABT2 rows (variable directions) or W.ctab (constant
+    // ones, stride 0), and the own reference component
+    cbase = tv >= 0 ? ABT.p0 + tv : W.ctab + cslot;
+    cstride = tv >= 0 ? ABT.stride : 0;
+    refp = stl ? xr + jx : ur + ju;
   };
   bind((int64_t)blockIdx.x * GROUPS + q);
-  const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
   // (Measured and dropped, round 4: stores from every lane with the masked-out ones into a
   // per-lane scratch, so that the waits for the prefetched loads no longer drain the stores --
   // 3.15 -> 4.73 ms, the scratch writes cost more than the drains; prefetching the backward
   // stages for every group: no change.)
-  // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
-  const int cslot = j < 3 ? j : j - 3;
   // s * blkdiag(Q, R) in LDS (shared by the wave's 4 instances): lane j reads column j (= row j),
   // the stage cost of direction j, when a backward stage needs it
   __shared__ T SW[NZ * NZ];
@@ -251,7 +282,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
   int kc = -1;                  // highest stage whose active set changed (group-uniform)
   int git = 0;                  // passes of the group's current instance
   bool u0fin = true;            // u0 of the flushed (final) pass is finite (staged outputs)
-  const bool stage_out = N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0;
+  // (the box kernel: always -- mpcb_create refuses box_u beyond N = 64 and mpcb_solve X / U that
+  // are not 16-B aligned -- so its stage loop carries no direct-store path)
+  const bool stage_out = BOX || (N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0);
   // an instance's outcome: the QP status of the unconstrained pass (P2 wrote it) carries over
   auto finish = [&]() {
     if (valid && j == NX) {
@@ -322,31 +355,34 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         wave_lds_sync();   // the stages' PX writes follow the reads
       }
       bool qp_ok = true;
-      // stage data one stage ahead: column j of [A|B], own (ybar - yref) and ybar components,
-      // own gap component
-      // (the prefetch keeps the raw loaded values: forming e = ybar - yref inside it made the
+      // Stage data one stage ahead (column j of [A|B], own ybar and yref components, own gap
+      // component) in two register slots, the stage loop unrolled by two (each slot a fixed register set: the
+      // copy of a one-slot prefetch into the stage's operands was 14 moves and 14 separate waits
+      // per stage).  Every group loads at every stage the wave visits, so no exec mask guards the
+      // loads: a group above its own restart stage (k > kc) reloads its stage kc, a cache hit,
+      // and discards the result.  (The prefetch keeps the raw loaded values: forming e = ybar - yref inside it made the
       // compiler wait for the loads it had just issued, vmcnt(0), at every backward stage)
-      T ncol[NX], nref, nyb, ngp = T(0);
-      auto bload = [&](int k) {
+      T rcol[2][NX], rref[2], ryb[2], rgp[2] = {T(0), T(0)};
+      const int kcl = kc >= 0 ? kc : 0;
+      auto bload = [&](int k, auto slot_tag) {
+        constexpr int sl = decltype(slot_tag)::value;
+        const int kk = k <= kc ? k : kcl;
         // column tv of the stage's ABT2 rows, or (constant directions) of W.ctab: one load
         // pattern for every lane (no lane branch)
-        const T* rows = tv >= 0 ? ABT.at(k) + tv : W.ctab + cslot;
+        const T* rows = cbase + (int64_t)kk * cstride;
 #pragma unroll
-        for (int i = 0; i < NX; ++i) ncol[i] = rows[i * ABT2_W];
-        nyb = XU.at(k)[j * SS];
-        nref = stl ? xr[(int64_t)k * NX + jx] : ur[(int64_t)k * NU + ju];
-        if (iterate) ngp = GP.at(k)[jx * SS];   // (input lanes: unused)
+        for (int i = 0; i < NX; ++i) rcol[sl][i] = rows[i * ABT2_W];
+        ryb[sl] = XU.at(kk)[j * SS];
+        rref[sl] = refp[(int64_t)kk * refs];
+        if (iterate) rgp[sl] = GP.at(kk)[jx * SS];   // (input lanes: unused)
       };
-      // (a group loads only the stages it recomputes, k <= kc: the others' results are discarded)
-      if (kmax <= kc) bload(kmax);
-      ASTAMP(0);
-      for (int k = kmax; k >= 0; --k) {
+      auto bstage = [&](int k, auto slot_tag) {
+        constexpr int sl = decltype(slot_tag)::value;
         const bool act = k <= kc;   // this group's stage is recomputed
         T col[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) col[i] = ncol[i];
-        const T e = nyb - nref, yb = nyb, gpo = ngp;
-        if (k > 0 && k - 1 <= kc) bload(k - 1);
+        for (int i = 0; i < NX; ++i) col[i] = rcol[sl][i];
+        const T e = ryb[sl] - rref[sl], yb = ryb[sl], gpo = rgp[sl];
         // pt = p + P gap (component j), h = [A|B]^T pt
         T pt = pj;
         if (iterate) {
@@ -415,30 +451,36 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
         });
         {
           const bool lo = (lowm >> k) & 1u, hi = (upm >> k) & 1u;
-          const int fx_own = (!stl && (lo || hi)) ? 1 : 0;
-          const T dl_own = lo ? (lbm - yb) : (hi ? (ubm - yb) : T(0));   // input lanes: yb = ubar
-          int fixed[NU];
-          T delta[NU];
-          fixed[0] = bc<NX + 0>(fx_own); fixed[1] = bc<NX + 1>(fx_own);
-          fixed[2] = bc<NX + 2>(fx_own); fixed[3] = bc<NX + 3>(fx_own);
-          delta[0] = bc<NX + 0>(dl_own); delta[1] = bc<NX + 1>(dl_own);
-          delta[2] = bc<NX + 2>(dl_own); delta[3] = bc<NX + 3>(dl_own);
-          T hn[NU];
+          const bool fx = !stl && (lo || hi);
+          // (a stage at which no group of the wave fixes a component: the masking is the identity)
+          if (__builtin_amdgcn_ballot_w64(fx)) {
+            const int fx_own = fx ? 1 : 0;
+            // input lanes (yb = ubar): the fixed value's offset, 0 where the component is free
+            const T dl_own = lo ? (lbm - yb) : (hi ? (ubm - yb) : T(0));
+            int fixed[NU];
+            T delta[NU];
+            fixed[0] = bc<NX + 0>(fx_own); fixed[1] = bc<NX + 1>(fx_own);
+            fixed[2] = bc<NX + 2>(fx_own); fixed[3] = bc<NX + 3>(fx_own);
+            delta[0] = bc<NX + 0>(dl_own); delta[1] = bc<NX + 1>(dl_own);
+            delta[2] = bc<NX + 2>(dl_own); delta[3] = bc<NX + 3>(dl_own);
+            T hn[NU];
 #pragma unroll
-          for (int m = 0; m < NU; ++m) {
-            T acc = ht[m];
+            for (int m = 0; m < NU; ++m) {
+              // h_F += H_FA delta_A (delta = 0 on the free components: no select)
+              T acc = ht[m];
 #pragma unroll
-            for (int n = 0; n < NU; ++n) acc += fixed[n] ? Ht[m * NU + n] * delta[n] : T(0);
-            hn[m] = fixed[m] ? -delta[m] : acc;
-            Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
-          }
+              for (int n = 0; n < NU; ++n) acc = fma(Ht[m * NU + n], delta[n], acc);
+              hn[m] = fixed[m] ? -delta[m] : acc;
+              Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
+            }
 #pragma unroll
-          for (int m = 0; m < NU; ++m) {
-            ht[m] = hn[m];
+            for (int m = 0; m < NU; ++m) {
+              ht[m] = hn[m];
 #pragma unroll
-            for (int n = 0; n < NU; ++n) {
-              const bool f = fixed[m] || fixed[n];
-              Ht[m * NU + n] = f ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+              for (int n = 0; n < NU; ++n) {
+                const bool f = fixed[m] || fixed[n];
+                Ht[m * NU + n] = f ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+              }
             }
           }
         }
@@ -476,21 +518,23 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
           }
         }
         ASTAMP(2);
-        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip)
+        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip).  Lane
+        // c writes its entry (i, c) to PX[max(i, c) * 12 + min(i, c)], i descending, so where two
+        // lanes write one slot the owner's later write stays; every lane then reads its column
+        // from the same per-lane addresses (no lane-class selects, whose hoisted 64-bit masks
+        // were spilled scalar registers)
         if (stl) {
 #pragma unroll
-          for (int i = 0; i < NX; ++i) PX[j * NX + i] = Pn[i];
+          for (int i = NX - 1; i >= 0; --i) PX[sym[i]] = Pn[i];
         }
         wave_lds_sync();
         {
+          // (the input lanes' Pc and pj are never read -- P's rows 12..15 of the products and
+          // the broadcasts from lanes >= 12 are not summed -- so they take whatever comes)
           const uint64_t ma = lane_mask(act);
 #pragma unroll
-          for (int i = 0; i < NX; ++i) {
-            const T o = PX[i * NX + jx];
-            const T nv = csel(mst, csel(lane_mask(i <= j), Pn[i], o), T(0));
-            Pc[i] = csel(ma, nv, Pc[i]);
-          }
-          pj = csel(ma, csel(mst, pn, T(0)), pj);
+          for (int i = 0; i < NX; ++i) Pc[i] = csel(ma, PX[sym[i]], Pc[i]);
+          pj = csel(ma, pn, pj);
         }
         // packed snapshot of P_k, p_k for a later restart: slot d of lane j is P[j][(j + d) % 12],
         // the entry lane max(j, o) published above
@@ -499,13 +543,24 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
 #pragma unroll
           for (int d = 0; d < 7; ++d) {
             const int o = jx + d < NX ? jx + d : jx + d - NX;
-            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
+            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];   // (sym[o])
           }
           ps[7] = pj;
           if (act && valid && stl && k > 0) stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);
         }
         wave_lds_sync();
         ASTAMP(3);
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      bload(kmax, I0{});
+      ASTAMP(0);
+      for (int k = kmax; k >= 0; k -= 2) {
+        if (k > 0) bload(k - 1, I1{});
+        bstage(k, I0{});
+        if (k == 0) break;
+        if (k > 1) bload(k - 2, I0{});
+        bstage(k - 1, I1{});
       }
       if (!qp_ok) st = MPCB_STATUS_QP_FAIL;
     }
@@ -609,7 +664,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& a) {
       const T v = sum4(acc);
       const bool lo = !stl && ((lowm >> k) & 1u), hi = !stl && ((upm >> k) & 1u);
       T tol_mu = T(0);
-      if (BOX && __builtin_amdgcn_ballot_w64(lo || hi)) {   // wave-uniform: the DPP block needs whole rows
+      // the rounding bound of mu matters only where its sign is wrong for its side (elsewhere
+      // the test below fails whatever the tolerance): computed only when some lane of the wave
+      // has such a multiplier (wave-uniform: the DPP block needs whole rows)
+      if (BOX && __builtin_amdgcn_ballot_w64((lo && v < T(0)) || (hi && v > T(0)))) {
         T aa[4] = {T(fabs(r0)), T(0), T(0), T(0)};
         dot16abs(aa, zj, row);
         tol_mu = T(64) * eps * sum4(aa);

@@ -91,7 +91,7 @@ template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p3(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * MPCB_WT_MAX * 7) == hipSuccess ? 0 : -2;
 }
 extern "C" int mpcb_debug_stamps_as(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_astamps), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -2;

@@ -460,7 +460,7 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
       a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
       a.imajor = h->cfg.box_u ? 0 : 1;
-      a.AB = ((h->cfg.box_u && MPCB_AS_AB2) || h->small) ? ab : nullptr;
+      a.AB = h->small ? ab : nullptr;   // (the small-chunk path's column-ordered [A|B])
       a.ABT = (h->cfg.box_u || h->small || h->tin || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;
       a.GH = h->cfg.box_u ? a.ABT + (int64_t)N * nbp * ABT2_REC : nullptr;
       a.PS = h->cfg.box_u ? a.GH + (int64_t)N * nbp * GH2_REC : nullptr;

@@ -40,7 +40,9 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 #ifndef MPCB_WT_MAX
 #define MPCB_WT_MAX 32768
 #endif
-#define WT_TABLE(name) __device__ unsigned long long name[MPCB_WT_MAX * 5];
+// slots 5, 6 (entries MPCB_WT_MAX * (4 + slot) + wg): s_memtime, the shader-clock counter, at loop
+// start and end, so a wave's clock is (slot-6 - slot-5 cycles) / (its loop's realtime)
+#define WT_TABLE(name) __device__ unsigned long long name[MPCB_WT_MAX * 7];
 // slot 4 of the table (entries MPCB_WT_MAX * 4 + wg): the wave's HW_ID (SIMD, CU, SE) and XCC_ID
 #define WT_HW(name)                                                                 \
   {                                                                                 \
@@ -51,7 +53,11 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 #define WT(name, slot)                                                              \
   {                                                                                 \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                 \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < MPCB_WT_MAX) name[blockIdx.x * 4 + (slot)] = t_; \
+    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                     \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < MPCB_WT_MAX) {                      \
+      name[blockIdx.x * 4 + (slot)] = t_;                                           \
+      if ((slot) == 1 || (slot) == 2) name[MPCB_WT_MAX * (4 + (slot)) + blockIdx.x] = c_; \
+    }                                                                               \
   }
 #else
 #define WT_TABLE(name)

@@ -120,10 +120,7 @@ constexpr int ABT2_W = NVAR, KR2_W = 14, PS2_W = 8;
 static_assert(sizeof(Weights<float>::ctab) == NX * ABT2_W * sizeof(float), "ctab is one ABT2 record");
 // The active-set kernel's backward reads its [A|B] column out of the ABT2 rows (12 strided loads:
 // the masked backward recomputes ~2/3 of the stage-instances once, the forward passes read the
-// rows ~4 times), so P2 writes [A|B] once; MPCB_AS_AB2=1 restores the separate AB2 column export.
-#ifndef MPCB_AS_AB2
-#define MPCB_AS_AB2 0
-#endif
+// rows ~4 times), so P2 writes [A|B] once (round 3: a separate AB2 column export cost more).
 constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, GH2_REC = 4 * 20,
               PS2_REC = 12 * PS2_W;
 
@@ -159,7 +156,7 @@ struct SplitArgs {
                      // the same launch (row_riccati_kernel); 2: the same as two launches
                      // (MPCB_FUSE_P12=0)
   int fwd;           // 1: run P3 (trajectories or iterate mode); 0: P2 writes u0/status
-  int rm;            // 1: P2 writes the row-major exports (AB2, ABT2, GH2, KR2 in a.AB/a.ABT/a.GH/a.KR)
+  int rm;            // 1: P2 writes the row-major exports (ABT2, KR2, PS2 in a.ABT/a.KR/a.PS)
   int imajor;        // row-major exports instance-major (an instance's N records contiguous: the
                      // unconstrained fp64 forward, measured -2 % per c2 step) or stage-major (the box
                      // path: P2's scattered export stores measured 10 % slower instance-major at c4)

@@ -40,7 +40,7 @@ template <class T> hipError_t launch_nominal_row(const SplitArgs<T>& a, hipStrea
 template hipError_t launch_nominal_row<double>(const SplitArgs<double>&, hipStream_t);
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p1(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 7) == hipSuccess ? 0 : -2;
 }
 #endif
 template hipError_t launch_nominal_row<float>(const SplitArgs<float>&, hipStream_t);

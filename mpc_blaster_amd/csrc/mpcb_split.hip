@@ -443,7 +443,7 @@ __device__ __forceinline__ void nominal_quad(const SplitArgs<T>& a) {
   xus.flush(lane, soa(a.XU, N, XU_REC, nb, c0), nqv);
 }
 
-// EXPORT: code for storing column j of [A|B] (a.AB, a.ABT) and the input rows of the stage
+// EXPORT: code for storing column j of [A|B] (a.ABT) and the input rows of the stage
 // Hessian (a.GH) for the 16-lane forward / active-set kernels; each store runs only when its
 // array is set (a separate export-free fp32 instantiation keeps the plain pass's registers lean)
 // ITER: iterate mode as a template argument (MPCB_P2_ITER_T, default on): the rollout-mode
@@ -624,24 +624,12 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       }
       STAMP(1);
       const int tv = tvj;   // exported: the state-dependent columns only
-      if (EXPORT && a.rm) {           // row-major exports (mpcb_kernels.h AB2_REC ...)
-        if (a.AB && valid && tv >= 0) stv<T, NX>(rec2(a.AB, k, AB2_REC, nb, c, N, a.imajor) + tv * NX, col);
-        if (!TIN && a.ABT && valid && tv >= 0) {
-          T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor);
+      // row-major ABT2 rows of the variable columns for the 16-lane forward pass / the active-set
+      // kernel (a.ABT is set exactly when a row-major consumer runs; TIN: the rollout wrote them)
+      if (!TIN && EXPORT && a.ABT && valid && tv >= 0) {
+        T* abt = rec2(a.ABT, k, ABT2_REC, nb, c, N, a.imajor);
 #pragma unroll
-          for (int i = 0; i < NX; ++i) abt[i * ABT2_W + tv] = col[i];
-        }
-      } else {
-        if (EXPORT && a.AB && valid && tv >= 0) {
-          T* ab = soa(a.AB, k, AB_REC, nb, c);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) ab[(i * NVAR + tv) * SS] = col[i];
-        }
-        if (!TIN && EXPORT && a.ABT && valid && tv >= 0) {
-          T* abt = soa(a.ABT, k, AB_REC, nb, c);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) abt[(tv * NX + i) * SS] = col[i];
-        }
+        for (int i = 0; i < NX; ++i) abt[i * ABT2_W + tv] = col[i];
       }
       if constexpr (!D64) {
         T pt = pj;
@@ -1234,10 +1222,10 @@ template int64_t split_elems_per_instance<float>(int, int, int);
 // (same translation unit as g_stamps: the library is built without -fgpu-rdc)
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p1f(unsigned long long* out) {   // the row body inside row_riccati_kernel
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p1), sizeof(unsigned long long) * MPCB_WT_MAX * 7) == hipSuccess ? 0 : -2;
 }
 extern "C" int mpcb_debug_wt_p2(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * MPCB_WT_MAX * 5) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::g_wt_p2), sizeof(unsigned long long) * MPCB_WT_MAX * 7) == hipSuccess ? 0 : -2;
 }
 #endif
 extern "C" int mpcb_debug_wt_max(void) { return MPCB_WT_MAX; }

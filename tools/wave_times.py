@@ -25,18 +25,20 @@ for _ in range(5):
     m.solve(d['x0'], d['xref'], d['uref'], want_traj=True)
 torch.cuda.synchronize()
 lib = _lib.load()
+lib.mpcb_debug_wt_max.restype = ctypes.c_int
+WMAX = lib.mpcb_debug_wt_max()   # table stride (mpcb_common.h MPCB_WT_MAX)
 waves = B // 4
 starts = {}
 # (c2 runs P1 inside row_riccati_kernel: its table is p1f; MPCB_FUSE_P12=0 builds: p1)
 for name in ('p1f' if os.environ.get('WT_P1', 'p1f') == 'p1f' else 'p1', 'p2', 'p3'):
-    buf = (ctypes.c_ulonglong * (4096 * 5))()
+    buf = (ctypes.c_ulonglong * (WMAX * 7))()
     f = getattr(lib, f'mpcb_debug_wt_{name}')
     name = name[:2]
     f.argtypes = [ctypes.c_void_p]
     assert f(buf) == 0
     raw = np.array(buf, dtype=np.uint64)
-    hw = raw[4096 * 4:4096 * 4 + waves]
-    t = raw[:4096 * 4].astype(np.float64).reshape(4096, 4)[:waves] * 0.01   # us
+    hw = raw[WMAX * 4:WMAX * 4 + waves]
+    t = raw[:WMAX * 4].astype(np.float64).reshape(WMAX, 4)[:waves] * 0.01   # us
     t0 = t[:, 0].min()
     starts[name] = (t0, t[:, 3].max())
     r = t - t0

@@ -34,7 +34,7 @@ waves = min(B, chunk) // 4
 assert waves <= WMAX
 f = lib.mpcb_debug_wt_p2
 f.argtypes = [ctypes.c_void_p]
-buf = (ctypes.c_ulonglong * (WMAX * 5))()
+buf = (ctypes.c_ulonglong * (WMAX * 7))()
 for _ in range(3):
     m.solve(d['x0'], d['xref'], d['uref'], wind=d['wind'], want_traj=W == 'c3')
 torch.cuda.synchronize()
@@ -59,6 +59,8 @@ for rep in range(REPS):
     key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
     ukey, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
     loop = r[:, 2] - r[:, 1]
+    cyc = (raw[WMAX * 6:WMAX * 6 + waves].astype(np.float64) - raw[WMAX * 5:WMAX * 5 + waves].astype(np.float64))
+    mhz = cyc / np.maximum(loop, 1e-3)   # shader-clock cycles per microsecond of each wave's loop
     life = r[:, 3] - r[:, 0]
     span = r[:, 3].max()
     # per-SIMD: its last exit and the sum of its waves' lifetimes
@@ -78,5 +80,8 @@ for rep in range(REPS):
           f'life med {np.median(life):5.1f} | SIMD last-exit p50 {np.median(last):6.1f} min {last.min():6.1f} | '
           f'resident at mid {np.bincount(conc.astype(int)).tolist()} | last wave: xcc {int(xcc[ilast])} '
           f'simd-waves {int(cnt[inv[ilast]])} entry {r[ilast, 0]:6.1f}')
+    print(f'    clock (s_memtime / s_memrealtime over each loop) MHz: median {np.median(mhz):6.0f} '
+          f'p5 {np.percentile(mhz, 5):6.0f} p95 {np.percentile(mhz, 95):6.0f} | loop cycles median {np.median(cyc):8.0f} '
+          f'p95 {np.percentile(cyc, 95):8.0f} | by XCD MHz: ' + ' '.join(f'{np.median(mhz[kx == x]):5.0f}' for x in range(8)))
     print('    XCD last exit: ' + ' '.join(f'{v:6.1f}' for v in xend) +
           ' | entries p50 by XCD: ' + ' '.join(f'{np.median(r[kx == x, 0]):6.1f}' for x in range(8)))
