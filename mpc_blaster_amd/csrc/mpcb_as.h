@@ -163,6 +163,22 @@ template <bool W32> struct Masks {
 #ifdef MPCB_AS_STAMPS
 WT_TABLE(g_wt_p3)
 #endif
+// (I <= jj) ? a : b with the lane condition computed at use into VCC (no hoisted lane mask)
+template <int I> __device__ __forceinline__ float sel_le(int jj, float a, float b) {
+  float r;
+  asm("v_cmp_le_i32 vcc, %3, %4\n\tv_cndmask_b32 %0, %2, %1, vcc" : "=v"(r) : "v"(a), "v"(b), "i"(I), "v"(jj) : "vcc");
+  return r;
+}
+template <int I> __device__ __forceinline__ double sel_le(int jj, double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  unsigned lo, hi;
+  asm("v_cmp_le_i32 vcc, %6, %7\n\tv_cndmask_b32 %0, %3, %2, vcc\n\tv_cndmask_b32 %1, %5, %4, vcc"
+      : "=&v"(lo), "=&v"(hi)
+      : "v"((unsigned)ua), "v"((unsigned)ub), "v"((unsigned)(ua >> 32)), "v"((unsigned)(ub >> 32)), "i"(I), "v"(jj)
+      : "vcc");
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // p as an opaque VGPR value that still addresses global memory (the address-space cast keeps the
 // loads and stores global_*: through a plain opaque pointer the compiler falls back to flat_*
 // accesses, which also count against lgkmcnt)
@@ -198,10 +214,6 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   const bool stl = j < NX;                          // state lane (else input lane ju)
   const uint64_t mst = lane_mask(stl);
   T* const PX = lds_px[q];
-  // the group's LDS slot of P's entry (i, jx): max(i, jx) * 12 + min(i, jx)
-  int sym[NX];
-#pragma unroll
-  for (int i = 0; i < NX; ++i) sym[i] = (i > jx ? i : jx) * NX + (i > jx ? jx : i);
   const int64_t nb = a.nb;
   const int N = a.N;
   // the RK4 tangent's position entry of a velocity column, h/6 * (1 + 2 + 2 + 1) as the tangent
@@ -213,7 +225,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   const T lbm = W.lbu[ju], ubm = W.ubu[ju];
   constexpr T eps = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920929e-7);
   const T tol_u = T(16) * eps * (fabs(lbm) + fabs(ubm) + T(1));
-  const int64_t nq = (nb + SS - 1) / SS;
+  int64_t nq = (nb + SS - 1) / SS;
+  // (box kernel, rollout mode: the record strides derived from nq are loop-invariant VGPRs too)
+  if constexpr (BOX && !ITER) asm volatile("" : "+v"(nq));   // (iterate: VGPR-bound already)
   // The group's instance and its workspace records.  Box kernel with a work counter (a.as_queue):
   // the grid holds the waves the machine keeps resident, and a group whose instance finished
   // takes the next one from the counter, so a wave does not carry three idle groups while its
@@ -518,22 +532,25 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
           }
         }
         ASTAMP(2);
-        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip).  Lane
-        // c writes its entry (i, c) to PX[max(i, c) * 12 + min(i, c)], i descending, so where two
-        // lanes write one slot the owner's later write stays; every lane then reads its column
-        // from the same per-lane addresses (no lane-class selects, whose hoisted 64-bit masks
-        // were spilled scalar registers)
+        // symmetric by construction: entry (r, c) from lane max(r, c) (see mpcb_split.hip): lane j
+        // publishes its column as row j of PX and takes the entries below its diagonal from the
+        // rows of the lanes that own them.  The lane-class select computes its condition at use
+        // (v_cmp into VCC): the twelve hoisted 64-bit masks of a plain select were spilled scalar
+        // registers, and per-lane LDS addresses instead of selects (measured) put 44 % of the
+        // kernel's LDS cycles into bank conflicts
         if (stl) {
 #pragma unroll
-          for (int i = NX - 1; i >= 0; --i) PX[sym[i]] = Pn[i];
+          for (int i = 0; i < NX; ++i) PX[j * NX + i] = Pn[i];
         }
         wave_lds_sync();
         {
           // (the input lanes' Pc and pj are never read -- P's rows 12..15 of the products and
           // the broadcasts from lanes >= 12 are not summed -- so they take whatever comes)
           const uint64_t ma = lane_mask(act);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) Pc[i] = csel(ma, PX[sym[i]], Pc[i]);
+          static_for<NX>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            Pc[i] = csel(ma, sel_le<i>(jx, Pn[i], PX[i * NX + jx]), Pc[i]);
+          });
           pj = csel(ma, pn, pj);
         }
         // packed snapshot of P_k, p_k for a later restart: slot d of lane j is P[j][(j + d) % 12],
@@ -543,7 +560,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
 #pragma unroll
           for (int d = 0; d < 7; ++d) {
             const int o = jx + d < NX ? jx + d : jx + d - NX;
-            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];   // (sym[o])
+            ps[d] = PX[(o > jx ? o : jx) * NX + (o > jx ? jx : o)];
           }
           ps[7] = pj;
           if (act && valid && stl && k > 0) stv<T, PS2_W>(PS.at(k) + j * PS2_W, ps);

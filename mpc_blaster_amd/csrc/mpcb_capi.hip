@@ -459,6 +459,8 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // row-major exports for the active-set kernel and the 16-lane forward pass; the optional
       // small-batch path (lin_kernel + box_body) keeps its own quad-blocked pair
       a.rm = (h->cfg.box_u || (h->fwd16 && a.fwd)) ? 1 : 0;
+      // (box path stage-major: instance-major exports measured no faster at c4 in round 5 --
+      // active-set kernel 3.15 vs 3.19 ms, P2 1.06-1.08 vs 1.04 ms -- and round 3)
       a.imajor = h->cfg.box_u ? 0 : 1;
       a.AB = h->small ? ab : nullptr;   // (the small-chunk path's column-ordered [A|B])
       a.ABT = (h->cfg.box_u || h->small || h->tin || (h->fwd16 && a.fwd)) ? ab + (int64_t)N * nbp * AB2_REC : nullptr;

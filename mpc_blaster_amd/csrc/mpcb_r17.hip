@@ -1277,8 +1277,8 @@ __global__ void __launch_bounds__(64) riccati17q_kernel(FullArgs<T> a) {
         else early = true;
         done = true;
       }
-      nshort = (alpha < T(IPM17_SHORT)) ? nshort + 1 : 0;
-      if (!done && (alpha < T(IPM17_STALL) || nshort >= IPM17_SHORT_RUN)) {
+      nshort = (alpha < T(sbox ? IPM17_SBOX_SHORT : IPM17_SHORT)) ? nshort + 1 : 0;
+      if (!done && (alpha < T(IPM17_STALL) || nshort >= (sbox ? IPM17_SBOX_SHORT_RUN : IPM17_SHORT_RUN))) {
         // collapsed step, or a run of short ones: converged near the solution (conditioning
         // limit), else an infeasible QP
         if (mu > ipm_brk || res > ipm_res) st = MPCB_STATUS_QP_FAIL;

@@ -265,6 +265,12 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
 # (test_gpu_full17.py::test_solve17_state_box_thin_interior_instance_converges).
 IPM_SIGMA_MIN, IPM_SIGMA_MAX, IPM_TAU, IPM_THETA, IPM_TOL, IPM_BREAK_TOL, IPM_STALL = 0.05, 0.9, 0.995, 0.1, 1e-12, 1e-5, 1e-6
 IPM_SHORT, IPM_SHORT_RUN = 1e-2, 10   # steps below 1e-2 ten times in a row: a stalled (infeasible) QP
+# ... with the state box (the only QPs that can be infeasible): 7 steps in a row below 0.05 while
+# not near the solution.  Chosen on the oracle's traces of the 4096 bench draws (tools/bench_full17.py,
+# N = 60): no LP-feasible instance takes more than 3 such steps in a row; the 68 LP-infeasible ones
+# now stop after at most 69 iterations (was 114; the feasible maximum is 62): the tail of the
+# device launch (tools/sbox_stall_study.py)
+IPM_SBOX_SHORT, IPM_SBOX_SHORT_RUN = 5e-2, 7
 
 
 def _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lbx=None, ubx=None, trace=None):
@@ -294,9 +300,10 @@ def _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60
     Newton system stops being positive definite once mu <= IPM_BREAK_TOL (an active row with
     lambda / s ~ 1e18: the current iterate is kept and counts as converged; likewise a step
     alpha < IPM_STALL there), or on a failure: a step alpha < IPM_STALL before that, or
-    IPM_SHORT_RUN steps in a row shorter than IPM_SHORT (an infeasible QP: on 256 random
-    state-box instances the feasible ones never took two such steps in a row, the LP-infeasible
-    ones 14-85), or a non-finite iterate, or after ``max_iter`` iterations.  Returns dx, du, status, iterations."""
+    IPM_SBOX_SHORT_RUN steps in a row shorter than IPM_SBOX_SHORT (an infeasible QP: on the 4096
+    bench draws no LP-feasible instance took more than 3 such steps in a row away from the
+    solution; without a state box IPM_SHORT_RUN / IPM_SHORT), or a non-finite iterate, or after
+    ``max_iter`` iterations.  Returns dx, du, status, iterations."""
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
     lbu = np.asarray(spec.lbu, dtype=np.float64) - ubar      # input rows, du coordinates
@@ -428,8 +435,9 @@ def _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60
         # a collapsed step ends the instance: near the solution (mu <= IPM_BREAK_TOL, feasible) the
         # Newton direction has reached the conditioning limit and the iterate counts as converged;
         # earlier it means an infeasible QP (the residual cannot reach zero)
-        nshort = np.where(alpha < IPM_SHORT, nshort + 1, 0)
-        stall = act & ((alpha < IPM_STALL) | (nshort >= IPM_SHORT_RUN))
+        short, short_run = (IPM_SBOX_SHORT, IPM_SBOX_SHORT_RUN) if sx else (IPM_SHORT, IPM_SHORT_RUN)
+        nshort = np.where(alpha < short, nshort + 1, 0)
+        stall = act & ((alpha < IPM_STALL) | (nshort >= short_run))
         near = (mu <= IPM_BREAK_TOL) & (res <= 1e-9)
         conv |= stall & near
         ok &= ~(stall & ~near)
@@ -472,9 +480,10 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
     Newton system stops being positive definite once mu <= IPM_BREAK_TOL (an active row with
     lambda / s ~ 1e18: the current iterate is kept and counts as converged; likewise a step
     alpha < IPM_STALL there), or on a failure: a step alpha < IPM_STALL before that, or
-    IPM_SHORT_RUN steps in a row shorter than IPM_SHORT (an infeasible QP: on 256 random
-    state-box instances the feasible ones never took two such steps in a row, the LP-infeasible
-    ones 14-85), or a non-finite iterate, or after ``max_iter`` iterations.  Returns dx, du, status, iterations."""
+    IPM_SBOX_SHORT_RUN steps in a row shorter than IPM_SBOX_SHORT (an infeasible QP: on the 4096
+    bench draws no LP-feasible instance took more than 3 such steps in a row away from the
+    solution; without a state box IPM_SHORT_RUN / IPM_SHORT), or a non-finite iterate, or after
+    ``max_iter`` iterations.  Returns dx, du, status, iterations."""
     if lbx is None:   # the input box alone: Mehrotra's predictor-corrector (_ipm_box_mehrotra)
         return _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=max_iter, trace=trace)
     Bsz, N = xbar.shape[0], spec.N
@@ -581,8 +590,9 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
         # a collapsed step ends the instance: near the solution (mu <= IPM_BREAK_TOL, feasible) the
         # Newton direction has reached the conditioning limit and the iterate counts as converged;
         # earlier it means an infeasible QP (the residual cannot reach zero)
-        nshort = np.where(alpha < IPM_SHORT, nshort + 1, 0)
-        stall = act & ((alpha < IPM_STALL) | (nshort >= IPM_SHORT_RUN))
+        short, short_run = (IPM_SBOX_SHORT, IPM_SBOX_SHORT_RUN) if sx else (IPM_SHORT, IPM_SHORT_RUN)
+        nshort = np.where(alpha < short, nshort + 1, 0)
+        stall = act & ((alpha < IPM_STALL) | (nshort >= short_run))
         near = (mu <= IPM_BREAK_TOL) & (res <= 1e-9)
         conv |= stall & near
         ok &= ~(stall & ~near)

@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--bounds', default='none', choices=['none', 'input', 'all'],
                     help="the reference's controlBound (input) and statesBound (all) by the interior point")
+    ap.add_argument('--dump', default=None, help='save per-instance status and QP statistics (npz)')
     args = ap.parse_args()
     import torch
     from mpc_blaster_amd import BatchedMPC, MPCConfig
@@ -105,6 +106,9 @@ def main():
     it_fl = fl + 2 * 12 * rows + ((2 * nz_ * nx_ + 2 * nu_ * nu_ + 4 * nx_ * nu_ + fwd) if meh else 0)
     pol_fl = fl + 12 * rows
     qp = None
+    if args.dump:
+        np.savez(args.dump, status=outs[3].cpu().numpy(),
+                 qp_stats=m.qp_stats(B).cpu().numpy() if box else np.zeros((B, 2), np.int32))
     if box:
         st = m.qp_stats(B).double().cpu().numpy()
         qp = dict(mean_iters=float(st[:, 0].mean()), max_iters=int(st[:, 0].max()),
