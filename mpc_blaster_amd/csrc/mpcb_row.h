@@ -131,15 +131,8 @@ __device__ __forceinline__ void tan_stage(const StageSc<T>& c, const T* __restri
 // one basic block; no captured-scalar record (CC) is written.
 // The body of P1 (nominal_row_kernel, and the first half of the fused row_riccati_kernel of
 // mpcb_split.hip).  The including translation unit declares WT_TABLE(g_wt_p1).
-// What the fused Riccati pass of the same wave (row_riccati_kernel, rollout mode) takes over
-// from the rollout's last interval through LDS instead of reading it back from the workspace after
-// a fence: lane t's slot of HAND_W values -- column t of [A_{N-1} | B_{N-1}] (TAN, 0..11), its
-// component of (xbar_{N-1} | ubar_{N-1}) (12) and of xbar_N (13) -- so the Riccati prologue waits
-// for none of the rollout's stores.  (In registers the values stayed live through the whole
-// rollout loop: +26 VGPRs, spilled to AGPRs.)
-constexpr int HAND_W = 14;
 template <class T, bool ITER, bool DJ, bool TAN>
-__device__ __forceinline__ void row_body(const SplitArgs<T>& a, T* hand = nullptr) {
+__device__ __forceinline__ void row_body(const SplitArgs<T>& a) {
   WT(g_wt_p1, 0);
   const int lane = threadIdx.x;
   const int t = lane & 15;                 // row lane
@@ -280,7 +273,6 @@ __device__ __forceinline__ void row_body(const SplitArgs<T>& a, T* hand = nullpt
     if (ITER && t < NX && k) X = lxq[k * NX + t];
     if (t >= NX) X = luq[k * NU + (t - NX)];
     xu0[k * xu_k + t * SS] = X;
-    if (hand && k == N - 1) hand[lane * HAND_W + 12] = X;
     // per-interval constants: the inputs, the thrust scale and J^-1 M(u) + the constant forces
     const T u0 = rbc<12>(X), u1 = rbc<13>(X), u2 = rbc<14>(X), u3 = rbc<15>(X);
     const T s = ((u0 + u1) + (u2 + u3) + M.t_blast) * M.minv;
@@ -437,12 +429,6 @@ __device__ __forceinline__ void row_body(const SplitArgs<T>& a, T* hand = nullpt
         for (int i = 0; i < NX; ++i) abt[i * ABT2_W] = dN[i];
       }
     }
-    if constexpr (TAN) {
-      if (hand && k == N - 1) {
-#pragma unroll
-        for (int i = 0; i < NX; ++i) hand[lane * HAND_W + i] = dN[i];
-      }
-    }
     if (ITER) {
       if (t < NX) gp0[k * gp_k + t * SS] = Xn - lxq[(k + 1) * NX + t];
     } else if (t < NX) {
@@ -456,12 +442,11 @@ __device__ __forceinline__ void row_body(const SplitArgs<T>& a, T* hand = nullpt
     X = T(0);
   }
   xu0[N * xu_k + t * SS] = X;
-  if (hand) hand[lane * HAND_W + 13] = X;
   WT(g_wt_p1, 3);
 }
 
 // dynamic LDS of the row rollout: the wave's staged u (and, iterate mode, xbar) records
-template <class T> __host__ __device__ static size_t row_lds_bytes(const SplitArgs<T>& a) {
+template <class T> static size_t row_lds_bytes(const SplitArgs<T>& a) {
   return (size_t)GROUPS * ((size_t)a.N * NU + (a.mode == MPCB_MODE_ITERATE ? (size_t)(a.N + 1) * NX : 0)) * sizeof(T);
 }
 

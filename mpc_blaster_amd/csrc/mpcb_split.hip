@@ -472,8 +472,7 @@ template <int L> __device__ __forceinline__ double rbc64(double v) {
 
 WT_TABLE(g_wt_p2)
 template <class T, bool EXPORT, bool ITER = false, bool TIN = false>
-__device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw,
-                                             const T* hand = nullptr) {
+__device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_t c_raw) {
   WT(g_wt_p2, 0);
   WT_HW(g_wt_p2);
   // fp64 DPP path: every exchange of the stage by row broadcasts -- Y reads P straight out of
@@ -530,8 +529,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
   T pj;      // p_{k+1}[j]
   T Pc[NX];  // column j of P_{k+1} (zero in the input lanes: P padded to 16x16)
   {
-    // (fused with the rollout: xbar_N is this lane's own last rollout value)
-    const T xN = hand ? hand[lane * HAND_W + 13] : soa(a.XU, N, XU_REC, nb, c)[jx * SS];
+    const T xN = soa(a.XU, N, XU_REC, nb, c)[jx * SS];
     L.v[j] = (j < NX) ? xN - xr[(int64_t)N * NX + jx] : T(0);
     wave_lds_sync();
     T acc = T(0);
@@ -597,16 +595,7 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
       asm volatile("" : "+v"(sw[i]));
     }
   }
-  if (hand) {   // stage N - 1 from the rollout's LDS hand-over (the same lane computed it)
-    if constexpr (TIN) {
-#pragma unroll
-      for (int i = 0; i < NX; ++i) pc[i] = hand[lane * HAND_W + i];
-    }
-    pyb = hand[lane * HAND_W + 12];
-    pyr = *((j < NX) ? xr + (int64_t)(N - 1) * NX + jx : ur + (int64_t)(N - 1) * NU + ju);
-  } else {
-    prefetch(N - 1);
-  }
+  prefetch(N - 1);
   commit(0);
   T cyb = pyb, cyr = pyr;
   int buf = 0;
@@ -619,12 +608,6 @@ __device__ __forceinline__ void riccati_body(const SplitArgs<T>& a, const int64_
     if constexpr (TIN) {
 #pragma unroll
       for (int i = 0; i < NX; ++i) col[i] = fma(kvar, pc[i], ce[i]);
-    }
-    if (hand && k == N - 1) {
-      // the first read of the rollout's stores (stage N - 2): ordered after them here, one
-      // stage into the recursion, by when they have long completed
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     if (k > 0) prefetch(k - 1);
     STAMP(0);
@@ -1116,23 +1099,12 @@ __global__ void __launch_bounds__(64) MPCB_P2_WAVES riccati_kernel_f64(SplitArgs
 #ifndef MPCB_FUSE_P12
 #define MPCB_FUSE_P12 1
 #endif
-// rollout mode: stage N - 1 and xbar_N handed over in LDS after the row body's staged inputs
-// (mpcb_row.h HAND_W; the fence before the Riccati pass's first workspace read moves into its
-// loop); iterate mode: the fence between the two bodies (its larger staging leaves no room)
-#ifndef MPCB_ROW_HAND
-#define MPCB_ROW_HAND 1
-#endif
 template <bool ITER, bool DJ>
 __global__ void __launch_bounds__(64) MPCB_P2_WAVES row_riccati_kernel(SplitArgs<double> a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char rr_dyn[];
-  constexpr bool HAND = !ITER && MPCB_ROW_HAND;
-  double* const hand = HAND ? reinterpret_cast<double*>(rr_dyn + row_lds_bytes(a)) : nullptr;
-  row_body<double, ITER, DJ, true>(a, hand);
-  if constexpr (!HAND) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  }
-  riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4), hand);
+  row_body<double, ITER, DJ, true>(a);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  riccati_body<double, true, ITER, true>(a, (int64_t)blockIdx.x * GROUPS + (threadIdx.x >> 4));
 }
 
 template <class T, bool USE_CC, bool ITER>
@@ -1163,9 +1135,8 @@ template <class T> hipError_t launch_split(const SplitArgs<T>& a, hipStream_t st
     // (the phase events: "nominal" empty, "riccati" the fused kernel)
     if (ev) (void)hipEventRecord(ev[1], st);
     const dim3 grid((unsigned)((a.nb + SS - 1) / SS));
+    const size_t lds = row_lds_bytes(a);
     const bool it = a.mode == MPCB_MODE_ITERATE;   // (the row body's mode is always a template argument)
-    // (+ the rollout-mode hand-over slots, mpcb_row.h HAND_W)
-    const size_t lds = row_lds_bytes(a) + (it ? 0 : (size_t)WAVE * HAND_W * sizeof(T));
     if constexpr (sizeof(T) == 8) {
       if (!dry_run()) {
         static const hipError_t lds_ok = [] {
