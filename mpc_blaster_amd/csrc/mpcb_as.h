@@ -244,6 +244,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
   const int cslot = j < 3 ? j : j - 3;
   auto bind = [&](int64_t c_raw) {
+#ifdef MPCB_AS_ORDER_DBG   // (tools/ab_as_order.py)
+    if (a.as_order && c_raw < nb) c_raw = a.as_order[c_raw];
+#endif
     valid = c_raw < nb;
     c = valid ? c_raw : nb - 1;       // an empty group shadows the last instance
     b = a.b0 + c;

@@ -63,6 +63,7 @@ LaunchLog& launch_log() {
 
 struct mpcb_handle {
   mpcb_config cfg;
+  const int32_t* as_order_dbg = nullptr;   // (MPCB_AS_ORDER_DBG builds) the active-set kernel's order
   int device;
   int64_t max_batch;
   int grid;              // resident slots (one wavefront of GROUPS instances each)
@@ -370,6 +371,15 @@ extern "C" int mpcb_destroy(mpcb_handle* h) {
   return MPCB_OK;
 }
 
+#ifdef MPCB_AS_ORDER_DBG
+// A/B of the active-set kernel's work order: a device array mapping the counter's tickets to
+// instances of the first chunk (nullptr: identity)
+extern "C" int mpcb_debug_set_as_order(mpcb_handle* h, const int32_t* dev_order) {
+  if (!h) return fail(MPCB_E_INVALID, "null handle");
+  h->as_order_dbg = dev_order;
+  return MPCB_OK;
+}
+#endif
 extern "C" int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* stream) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
   if (!h->qp_stats) return fail(MPCB_E_UNSUPPORTED, "QP statistics are kept by input-box handles");
@@ -470,6 +480,7 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // the active-set kernel's work counter (MPCB_AS_PERSIST=0: one wave per instance quad)
       a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
       if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
+      a.as_order = (h->cfg.box_u && b0 == 0) ? h->as_order_dbg : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);
       if (e != hipSuccess) return fail(MPCB_E_HIP, "split launch: %s", hipGetErrorString(e));

@@ -145,6 +145,7 @@ struct SplitArgs {
   int32_t* qp_stats; // box path (nullable): per global instance [forward passes, masked backward
                      // stages] until its active set converged
   int* as_queue;     // box path (nullable): the active-set kernel's work counter
+  const int32_t* as_order;   // (MPCB_AS_ORDER_DBG builds, nullable) ticket -> chunk instance
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

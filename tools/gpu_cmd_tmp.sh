@@ -1,6 +1,5 @@
 set -e
-O=gpurun_out/r05_b8; mkdir -p $O
+O=gpurun_out/r05_b9; mkdir -p $O
 export TMPDIR=/tmp
-bash tools/ab_c2.sh $O main nohand
-for ch in 65536 131072; do MPCB_CHUNK=$ch timeout -k 10 200 python bench.py --workload c5 --no-cpu-baseline > $O/c5_chunk$ch.log 2>&1; done
-echo b8_done
+MPCB_LIB=mpc_blaster_amd/variants/lib_asord.so timeout -k 10 300 python tools/ab_as_order.py 20 > $O/ab_as_order.txt 2>&1
+echo b9_done
