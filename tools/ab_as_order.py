@@ -55,9 +55,17 @@ rev = torch.flip(lpt, [0]).contiguous()
 run('lpt', lpt)
 run('random', rnd)
 run('spt', rev)
+# the hard instances first (longest first among them), the rest in index order (its locality)
+hard = {}
+for thr in (5, 6, 8):
+    h = np.nonzero(p > thr)[0]
+    h = h[np.argsort(-p[h], kind='stable')]
+    rest = np.nonzero(p <= thr)[0]
+    hard[thr] = torch.from_numpy(np.concatenate([h, rest]).astype(np.int32)).cuda()
+    run(f'hard>{thr}', hard[thr])
 run('index2', None)
 run('lpt2', lpt)
-for k in ('lpt', 'random', 'spt', 'index2', 'lpt2'):
+for k in ('lpt', 'random', 'spt', 'hard>5', 'hard>6', 'hard>8', 'index2', 'lpt2'):
     same = all(torch.equal(a, b) for a, b in zip(outs['index'], outs[k]))
     print(f'{k}: outputs bit-identical to index order: {same}')
 lib.mpcb_debug_set_as_order(m._h, None)
