@@ -63,9 +63,28 @@ for thr in (5, 6, 8):
     rest = np.nonzero(p <= thr)[0]
     hard[thr] = torch.from_numpy(np.concatenate([h, rest]).astype(np.int32)).cuda()
     run(f'hard>{thr}', hard[thr])
+# a predictor available before the active set: the unconstrained solution's box violation
+# (the same P2 gains and forward pass as the active set's first pass), largest first for the
+# top fraction, the rest in index order
+mu = BatchedMPC(MPCConfig(N=N, dtype='f32'), max_batch=B)
+mu.solve(d['x0'], d['xref'], d['uref'], want_traj=True)
+Uu = mu._U.double()
+mag = ((-Uu).clamp(min=0) + (Uu - 65.0).clamp(min=0)).sum(dim=(1, 2)).cpu().numpy()
+nv = ((Uu < 0) | (Uu > 65.0)).sum(dim=(1, 2)).cpu().numpy()
+mu.close()
+for nm, key in (('mag', mag), ('nv', nv)):
+    for frac in (0.03, 0.1):
+        kth = np.sort(key)[::-1][int(frac * B)]
+        h = np.nonzero(key > kth)[0]
+        h = h[np.argsort(-key[h], kind='stable')]
+        rest = np.nonzero(key <= kth)[0]
+        o = torch.from_numpy(np.concatenate([h, rest]).astype(np.int32)).cuda()
+        cap = (p[h] > 8).sum()
+        print(f'{nm} top {frac:.0%}: {len(h)} first, {cap} of {(p > 8).sum()} hard (>8 passes) among them')
+        run(f'{nm}{int(frac * 100)}', o)
 run('index2', None)
 run('lpt2', lpt)
-for k in ('lpt', 'random', 'spt', 'hard>5', 'hard>6', 'hard>8', 'index2', 'lpt2'):
+for k in ('lpt', 'random', 'spt', 'hard>5', 'hard>6', 'hard>8', 'mag3', 'mag10', 'nv3', 'nv10', 'index2', 'lpt2'):
     same = all(torch.equal(a, b) for a, b in zip(outs['index'], outs[k]))
     print(f'{k}: outputs bit-identical to index order: {same}')
 lib.mpcb_debug_set_as_order(m._h, None)
