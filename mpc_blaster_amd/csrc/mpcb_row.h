@@ -283,9 +283,12 @@ __device__ __forceinline__ void row_body(const SplitArgs<T>& a) {
     // angle addition at stages 1..3), so the four stages are one basic block in which the
     // scheduler interleaves the tangent of stage s with the sin/cos of stage s + 1 (a branch per
     // stage around the fallbacks kept them apart: P1 45 -> 39 us at c2).  It returns whether an
-    // angle lane was outside those ranges; the wave then recomputes the interval with SLOW = true
-    // (sc() and its fallback at every stage) before anything of the interval but the CC record,
-    // which the second pass rewrites, is stored.
+    // angle lane was outside those ranges; the instances (16-lane rows) with such a lane then
+    // recompute the interval with SLOW = true (sc() and its fallback at every stage) before
+    // anything of the interval but the CC record, which the second pass rewrites, is stored.  The
+    // redo runs under an exec mask of those rows only, so the other instances of the wave keep the
+    // fast pass's results bit for bit (a wave-wide redo made an instance's last bits depend on its
+    // wave-mates: tests/test_gpu_edges.py).
     auto interval = [&](auto slow_tag) -> bool {
       constexpr bool SLOW = decltype(slow_tag)::value;
       bool bad = false;
@@ -418,7 +421,10 @@ __device__ __forceinline__ void row_body(const SplitArgs<T>& a) {
       }
       return bad;
     };
-    if (__any(interval(std::false_type{}))) (void)interval(std::true_type{});
+    {
+      const uint64_t bad = __builtin_amdgcn_ballot_w64(interval(std::false_type{}));
+      if ((bad >> (lane & 48)) & 0xFFFFull) (void)interval(std::true_type{});
+    }
     if constexpr (TAN) {
       // column var_col(tv) of [A_k | B_k] into the ABT2 rows: entry (i, tv) at i * ABT2_W + tv.
       // (Staging the wave's four records in LDS and writing them as 16-B vectors measured the

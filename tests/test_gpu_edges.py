@@ -1,0 +1,139 @@
+"""GPU edge cases of the solve path through the C ABI: empty batches, a non-finite instance inside
+a batch, the shortest horizon and long horizons.
+
+* Empty batch: every path returns without launching anything and without an error.
+* A NaN in one instance's x0: that instance reports a non-OK status, and every other instance's
+  outputs are bit-identical to the same batch with a finite x0 in its place (instances are
+  independent on every path: the fused row kernel, the thread-per-instance forward, the
+  active-set work counter, the 17/6 interior point).  This found the row rollout's wave-wide
+  slow-path redo (mpcb_row.h), which changed the last bits of the NaN instance's wave-mates.
+* N = 1 and long horizons against the oracle at the fp64 bound of tests/test_gpu_parity.py
+  (1e-9 normwise); the long unconstrained horizon takes the two-launch fallback of the fused
+  kernel (its LDS staging exceeds the one-wave-per-SIMD share: mpcb_capi.hip select_path).
+"""
+import numpy as np
+import pytest
+
+from oracle.inputs import make_inputs
+from oracle.ocp import OcpSpec, mpc_solve
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+STATUS_OK = 0
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, dtype=np.float64).reshape(b.shape[0], -1)
+    return np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1.0)
+
+
+def _mpc(N, dtype, box, max_batch, env=None, monkeypatch=None):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    cfg = MPCConfig(N=N, dtype=dtype, lbu=np.zeros(4) if box else None,
+                    ubu=np.full(4, 65.0) if box else None)
+    return BatchedMPC(cfg, max_batch=max_batch)
+
+
+def _outputs(m):
+    torch.cuda.synchronize()
+    return [t.cpu().numpy().copy() for t in (m.get_control(), m.get_state_trajectory(),
+                                             m.get_input_trajectory(), m.get_status())]
+
+
+@pytest.mark.parametrize('N,dtype,box', [(20, 'f64', False), (20, 'f32', False), (30, 'f32', True)])
+def test_empty_batch_is_a_noop(N, dtype, box):
+    m = _mpc(N, dtype, box, 64)
+    x0 = np.zeros((0, 12))
+    xref = np.zeros((1, N + 1, 12))
+    uref = np.full((1, N, 4), 22.0725)
+    u0 = m.solve(x0, xref, uref)
+    torch.cuda.synchronize()
+    assert tuple(u0.shape) == (0, 4)
+    assert tuple(m.get_status().shape) == (0,)
+    if box:
+        assert tuple(m.qp_stats(0).shape) == (0, 2)
+    # and the handle still solves afterwards
+    inp = make_inputs('c4' if box else 'c2', ids=np.arange(5, dtype=np.uint64), N=N)
+    m.solve(inp['x0'], inp['xref'], inp['uref'])
+    assert (_outputs(m)[3] == STATUS_OK).all()
+
+
+@pytest.mark.parametrize('cfg,N,dtype,box,B', [
+    ('c2', 20, 'f64', False, 4096),    # fused row kernel + 16-lane forward
+    ('c2', 20, 'f64', False, 203),     # small-batch path
+    ('c3', 20, 'f32', False, 20000),   # thread-per-instance rollout / forward, captured-scalar P2
+    ('c4', 30, 'f32', True, 1000),     # P2 exports + active-set work counter
+    ('c4', 30, 'f64', True, 300),
+])
+def test_nonfinite_instance_is_flagged_and_isolated(cfg, N, dtype, box, B):
+    inp = make_inputs(cfg, ids=np.arange(B, dtype=np.uint64), N=N)
+    bad = [17, B - 2]
+    m = _mpc(N, dtype, box, B)
+    x_ok = inp['x0'].copy()
+    x_ok[bad] = x_ok[[b - 1 for b in bad]]
+    m.solve(x_ok, inp['xref'], inp['uref'])
+    ref = _outputs(m)
+    x_nan = inp['x0'].copy()
+    x_nan[bad[0], 3] = np.nan
+    x_nan[bad[1], 0] = np.inf
+    m.solve(x_nan, inp['xref'], inp['uref'])
+    got = _outputs(m)
+    st = got[3]
+    print(f'{cfg} {dtype} box={box} B={B}: status of the non-finite instances {st[bad].tolist()}')
+    assert (st[bad] != STATUS_OK).all()
+    keep = np.setdiff1d(np.arange(B), bad)
+    assert (st[keep] == STATUS_OK).all() and (ref[3] == STATUS_OK).all()
+    for name, a, b in zip(('u0', 'X', 'U'), got[:3], ref[:3]):
+        diff = np.nonzero((a[keep] != b[keep]).reshape(len(keep), -1).any(axis=1))[0]
+        if len(diff):
+            print(f'  {name}: {len(diff)} instances differ, e.g. {keep[diff[:12]].tolist()}, max abs '
+                  f'{np.abs(a[keep] - b[keep]).max():.3e}')
+    for a, b in zip(got[:3], ref[:3]):
+        assert np.array_equal(a[keep], b[keep])
+
+
+@pytest.mark.parametrize('N,box,path', [(1, False, None), (1, True, None), (1, False, 'split'),
+                                        (200, False, None), (200, False, 'split'), (64, True, None)])
+def test_horizon_extremes_match_oracle_fp64(N, box, path, monkeypatch):
+    B = 37 if path is None else 2048
+    cfg = 'c4' if box else 'c3'
+    inp = make_inputs(cfg, ids=np.arange(B, dtype=np.uint64), N=N)
+    env = {'MPCB_SPLIT_MIN_BATCH': '1'} if path == 'split' else {}
+    m = _mpc(N, 'f64', box, B, env, monkeypatch)
+    m.solve(inp['x0'], inp['xref'], inp['uref'])
+    u0, X, U, st = _outputs(m)
+    o = mpc_solve(inp['x0'], inp['xref'], inp['uref'],
+                  OcpSpec(N=N, lbu=np.zeros(4) if box else None, ubu=np.full(4, 65.0) if box else None))
+    e = max(relerr(u0, o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max())
+    print(f'N={N} box={box} path={path} B={B}: max rel err {e:.2e}')
+    assert (st == o['status']).all() and (st == STATUS_OK).all()
+    assert e < 1e-9
+
+
+@pytest.mark.parametrize('states', [False, True])
+def test_full17_nonfinite_instance_is_flagged_and_isolated(states):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    from test_gpu_full17 import LBU17, SB_HI, SB_LO, UBU17, _inputs
+    N, B = 20, 64
+    kw = dict(lbx=SB_LO, ubx=SB_HI) if states else {}
+    m = BatchedMPC(MPCConfig.full(N=N, lbu=LBU17, ubu=UBU17, **kw), max_batch=B)
+    x0, xref, uref, p = _inputs(B, N, 41)
+    m.set_params(p)
+    x_ok = x0.copy()
+    x_ok[9] = x_ok[8]
+    m.solve(x_ok, xref, uref)
+    ref = _outputs(m)
+    x_nan = x0.copy()
+    x_nan[9, 5] = np.nan
+    m.solve(x_nan, xref, uref)
+    got = _outputs(m)
+    print(f'17/6 boxes (states {states}): status of the non-finite instance {int(got[3][9])}')
+    assert got[3][9] != STATUS_OK
+    keep = np.setdiff1d(np.arange(B), [9])
+    assert (got[3][keep] == ref[3][keep]).all()
+    for a, b in zip(got[:3], ref[:3]):
+        assert np.array_equal(a[keep], b[keep])
