@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-phase device times of the in-tree library under environment overrides, alternating twice.
 # usage: tools/env_ab.sh OUTDIR WORKLOAD "NAME=ENV1 ENV2;NAME2=ENV3" [pytest -k expr]
-# e.g.   tools/env_ab.sh p1row c2 "quad=MPCB_ROW_P1_MAX=0;row=" "c2 or iterate"
+# e.g.   tools/env_ab.sh fuse c2 "two=MPCB_FUSE_P12=0;one=" "c2 or iterate"
 set -e
 O=gpurun_out/$1; mkdir -p $O; W=$2; CASES=$3; K=${4:-}
 export TMPDIR=/tmp
