@@ -67,7 +67,9 @@ typedef struct mpcb_config {
   int32_t N;             /* horizon (ocp.dims.N, blastermodel.py:226) */
   int32_t dtype;         /* MPCB_F64 | MPCB_F32 */
   int32_t box_u;         /* 1: lbu <= u <= ubu on stages 0..N-1 (idxbu, blastermodel.py:261) */
-  int32_t max_as_iter;   /* active-set / interior-point iteration cap for box_u */
+  int32_t max_as_iter;   /* box_u iteration cap.  17/6: interior-point iterations.  12/4: active-set
+                            passes, at most 48 (AS_IPM_AFTER); an instance not converged by then is
+                            solved by the interior point (<= 100 iterations, mpcb_asipm.h) */
   int32_t box_x;         /* 17/6 only, needs box_u: lbx <= x_k <= ubx on stages 1..N-1 (idxbx,
                             blastermodel.py:268-270 statesBound; JSON constraints.lbx/ubx) */
   int32_t reserved;

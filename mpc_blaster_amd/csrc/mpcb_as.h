@@ -199,7 +199,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     a.XU = vglobal(a.XU); a.GP = vglobal(a.GP); a.ABT = vglobal(a.ABT); a.GH = vglobal(a.GH);
     a.KR = vglobal(a.KR); a.PS = vglobal(a.PS); a.xref = vglobal(a.xref); a.uref = vglobal(a.uref);
     a.u0 = vglobal(a.u0); a.X = vglobal(a.X); a.U = vglobal(a.U); a.status = vglobal(a.status);
-    a.qp_stats = vglobal(a.qp_stats); a.x0 = vglobal(a.x0);
+    a.qp_stats = vglobal(a.qp_stats); a.x0 = vglobal(a.x0); a.as_fb = vglobal(a.as_fb);
   }
   using Mk = Masks<W32>;
   using M = typename Mk::M;
@@ -303,7 +303,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   // are not 16-B aligned -- so its stage loop carries no direct-store path)
   const bool stage_out = BOX || (N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0);
   // an instance's outcome: the QP status of the unconstrained pass (P2 wrote it) carries over
-  auto finish = [&]() {
+  auto finish = [&](bool write_status) {
     if (valid && j == NX) {
       bool fin = u0fin;
       if (!stage_out) {   // direct stores
@@ -313,7 +313,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         for (int m = 0; m < NU; ++m) fin = fin && isfin(u0c[m]);
       }
       const int32_t st0 = a.status[b];
-      a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
+      if (write_status) a.status[b] = !fin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);
       if (BOX && a.qp_stats) {
         a.qp_stats[2 * b] = n_fwd;
         a.qp_stats[2 * b + 1] = n_bst;
@@ -781,8 +781,16 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     ++git;
     if (fin_now) {
-      if (!gconv) st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
-      finish();
+      // not converged within the pass budget (min(max_as_iter, AS_IPM_AFTER), mpcb_capi.hip): the
+      // interior point takes the instance over (mpcb_asipm.h, oracle.ocp.pdas_solve) unless a
+      // factorisation failed; the status is then the fallback's to write
+      const bool to_ipm = BOX && !gconv && st == MPCB_STATUS_OK && a.as_fb;
+      if (to_ipm) {
+        if (j == 0) a.as_fb[2 + atomicAdd(a.as_fb, 1)] = (int)c;
+      } else if (!gconv) {
+        st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+      }
+      finish(!to_ipm);
       // the next instance of the chunk (lane 0 of the group draws it), else the group stays empty
       int nxt = (int)nb;
       if (a.as_queue) {
@@ -808,7 +816,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int i_ = 0; i_ < 12; ++i_) g_astamps[i_] = ast_acc[i_];
 #endif
-  if constexpr (!BOX) finish();   // (the box kernel finishes each instance as it converges)
+  if constexpr (!BOX) finish(true);   // (the box kernel finishes each instance as it converges)
   if constexpr (!BOX) AS_WT(3);
 }
 

@@ -25,6 +25,7 @@
 // needs all four) instead of in every lane.
 #define MPCB_AS_OWNER
 #include "mpcb_as.h"
+#include "mpcb_asipm.h"
 
 namespace mpcb {
 
@@ -35,6 +36,11 @@ template <bool W32, bool ITER = false>
 __global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true, W32, ITER>(a); }
 template <class T, bool ITER = false>
 __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false, false, ITER>(a); }
+template <class T, bool ITER = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 2 : 1, 8)))
+as_ipm_kernel(SplitArgs<T> a) {
+  asq::ipm_body<T, ITER>(a);
+}
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
@@ -49,6 +55,10 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
     }();
     if (g > resident) g = resident;
     const hipError_t e = hipMemsetAsync(a.as_queue, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+  }
+  if (a.as_fb && !dry_run()) {   // the interior-point fallback's list starts empty
+    const hipError_t e = hipMemsetAsync(a.as_fb, 0, 2 * sizeof(int), st);
     if (e != hipSuccess) return e;
   }
   const bool w32 = a.N <= 32;   // (the stage masks fit 32 bits)
@@ -69,6 +79,21 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
       if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<true>), dim3(g), dim3(64), lds, st, a);
       else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<false>), dim3(g), dim3(64), lds, st, a);
     }
+  }
+  // the instances the active set handed over (usually none: the waves read an empty list and
+  // exit).  Not in the launch log, which keeps the active-set kernel as the phase's kernel.
+  if (a.as_fb && !dry_run()) {
+    static const unsigned resident_ipm = [] {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      return (unsigned)cus * 4u * (sizeof(T) == 4 ? 2u : 1u);
+    }();
+    unsigned gi = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+    if (gi > resident_ipm) gi = resident_ipm;
+    if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((as_ipm_kernel<T, true>), dim3(gi), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((as_ipm_kernel<T, false>), dim3(gi), dim3(64), 0, st, a);
   }
   return dry_run() ? hipSuccess : hipGetLastError();
 }

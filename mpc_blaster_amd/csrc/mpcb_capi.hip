@@ -345,8 +345,9 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
     return fail(MPCB_E_HIP, "weights upload: %s", hipGetErrorString(e));
   }
   if (cfg->box_u && (full || h->split)) {
-    // (+ 16: the 12/4 active-set kernel's work counter after the statistics)
-    e = hipMalloc((void**)&h->qp_stats, ((size_t)max_batch * 2 + 16) * sizeof(int32_t));
+    // (+ 16: the 12/4 active-set kernel's work counter after the statistics; then its
+    // interior-point fallback's list, 2 + max_batch: SplitArgs::as_fb)
+    e = hipMalloc((void**)&h->qp_stats, ((size_t)max_batch * 3 + 18) * sizeof(int32_t));
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
       (void)hipFree(h->weights);
@@ -448,7 +449,8 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
     a.xbar = (const T*)xbar; a.ubar = (const T*)ubar;
     a.u0 = (T*)u0; a.X = (T*)X; a.U = (T*)U; a.status = status;
     a.fwd = (X || U || mode == MPCB_MODE_ITERATE || h->cfg.box_u) ? 1 : 0;
-    a.max_as_iter = h->cfg.max_as_iter;
+    // the active set's pass budget; instances still unconverged go to the interior point
+    a.max_as_iter = h->cfg.max_as_iter < AS_IPM_AFTER ? h->cfg.max_as_iter : AS_IPM_AFTER;
     const int N = h->cfg.N;
     int chunk_i = 0;
     for (int64_t b0 = 0; b0 < B; b0 += h->chunk) {
@@ -480,6 +482,7 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       // the active-set kernel's work counter (MPCB_AS_PERSIST=0: one wave per instance quad)
       a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
       if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
+      a.as_fb = (h->cfg.box_u && h->qp_stats) ? h->qp_stats + 2 * h->max_batch + 16 : nullptr;
       a.as_order = (h->cfg.box_u && b0 == 0) ? h->as_order_dbg : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);

@@ -124,6 +124,10 @@ static_assert(sizeof(Weights<float>::ctab) == NX * ABT2_W * sizeof(float), "ctab
 constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, GH2_REC = 4 * 20,
               PS2_REC = 12 * PS2_W;
 
+// the 12/4 input box: active-set passes before an unconverged instance goes to the interior-point
+// fallback (oracle.ocp.AS_IPM_AFTER; mpcb_asipm.h)
+constexpr int AS_IPM_AFTER = 48;
+
 template <class T>
 struct SplitArgs {
   int64_t b0;        // first global instance of the chunk
@@ -146,6 +150,8 @@ struct SplitArgs {
                      // stages] until its active set converged
   int* as_queue;     // box path (nullable): the active-set kernel's work counter
   const int32_t* as_order;   // (MPCB_AS_ORDER_DBG builds, nullable) ticket -> chunk instance
+  int* as_fb;        // box path (nullable): the interior-point fallback's list ([0] count, [2 + t]
+                     // chunk instance), filled by the active-set kernel (mpcb_asipm.h)
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

@@ -194,6 +194,16 @@ def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
     return dx, du, mu, ok
 
 
+# The 12/4 input box's fallback: an instance whose active set has not converged after
+# min(max_as_iter, AS_IPM_AFTER) passes is solved again by the interior point (ipm_box_solve with
+# the adaptive centring, input rows only, at most AS_IPM_ITERS iterations).  The least-index backup
+# rule terminates finitely but can need thousands of passes: with a +-5 N wind and sine references
+# (N = 18) 262 of 3000 instances took more than 60, one more than 1500, where the interior point
+# needs at most 24 iterations; on the c4 bench draws the active set needs at most 39 passes, so
+# the fallback never runs there.
+AS_IPM_AFTER, AS_IPM_ITERS = 48, 100
+
+
 def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int = 3):
     """Exact input-box QP: primal-dual active set with the Kim-Park block-principal-pivoting
     safeguard (finite termination for the SPD reduced Hessian, a P-matrix LCP).
@@ -204,7 +214,10 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     Full exchange of V while |V| keeps decreasing (or for ``pbar`` tries); otherwise only the
     element of V with the least index k*nu + m is exchanged (Murty's least-index backup rule,
     finite for a P-matrix LCP).  Measured on 2000 c4 instances: the least index converges in at
-    most 28 iterations where the largest index needs up to 132 (mean 3.8 vs 4.0).
+    most 28 iterations where the largest index needs up to 132 (mean 3.8 vs 4.0).  Instances not
+    converged after min(max_as_iter, AS_IPM_AFTER) passes are handed to the interior point (see
+    AS_IPM_AFTER); their status and solution are the interior point's, their iteration count the
+    passes plus its iterations.
     Returns dx, du, status, iterations.
     """
     Bsz, N = xbar.shape[0], spec.N
@@ -221,7 +234,7 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     out_dx = np.zeros((Bsz, N + 1, NX))
     out_du = np.zeros((Bsz, N, NU))
     flat_idx = np.arange(N * NU).reshape(N, NU)
-    for it in range(spec.max_as_iter):
+    for it in range(min(spec.max_as_iter, AS_IPM_AFTER)):
         fixed = low | up
         delta = np.where(low, lb - ubar, np.where(up, ub - ubar, 0.0))
         dx, du, mu, ok2 = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, fixed, delta)
@@ -252,6 +265,14 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
         up = np.where(sel & v_hi, True, np.where(sel & v_fu, False, up))
     status = np.where(done, STATUS_OK, STATUS_MAXITER).astype(np.int32)
     status = np.where(ok, status, STATUS_QP_FAIL).astype(np.int32)
+    fb = np.nonzero(~done & ok)[0]
+    if len(fb):   # the interior point's fallback
+        sub = lambda a: a[fb]
+        with np.errstate(all='ignore'):
+            fdx, fdu, fst, fit = ipm_box_solve(sub(A), sub(Bm), sub(gap), sub(dx0), sub(xbar), sub(ubar), sub(xref),
+                                               sub(uref), spec, max_iter=AS_IPM_ITERS, centring='adaptive')
+        out_dx[fb], out_du[fb], status[fb] = fdx, fdu, fst
+        iters[fb] += fit
     return out_dx, out_du, status, iters
 
 
@@ -459,7 +480,8 @@ def _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60
     return dx, du, status, it
 
 
-def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lbx=None, ubx=None, trace=None):
+def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lbx=None, ubx=None, trace=None,
+                  centring=None):
     """Box-constrained QP by a primal-dual interior point over the Riccati recursion (the method
     of acados' HPIPM; the full 17/6 model, where the active set above can need thousands of
     exchanges).  Constraint rows: the input box on stages 0..N-1 and, when ``lbx``/``ubx`` are
@@ -483,8 +505,10 @@ def ipm_box_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=60, lb
     IPM_SBOX_SHORT_RUN steps in a row shorter than IPM_SBOX_SHORT (an infeasible QP: on the 4096
     bench draws no LP-feasible instance took more than 3 such steps in a row away from the
     solution; without a state box IPM_SHORT_RUN / IPM_SHORT), or a non-finite iterate, or after
-    ``max_iter`` iterations.  Returns dx, du, status, iterations."""
-    if lbx is None:   # the input box alone: Mehrotra's predictor-corrector (_ipm_box_mehrotra)
+    ``max_iter`` iterations.  Returns dx, du, status, iterations.
+    ``centring='adaptive'`` keeps this scheme for the input box alone (the 12/4 active set's
+    fallback, pdas_solve); otherwise the input box alone takes Mehrotra's predictor-corrector."""
+    if lbx is None and centring != 'adaptive':   # the input box alone: _ipm_box_mehrotra
         return _ipm_box_mehrotra(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, max_iter=max_iter, trace=trace)
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]

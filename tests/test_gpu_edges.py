@@ -164,3 +164,41 @@ def test_batch_order_invariance(cfg, N, dtype, box, B):
             print(f'{cfg}: {name} differs on {len(d)} instances, e.g. {d[:12].tolist()}')
         assert same
     assert (fwd[3] == STATUS_OK).all()
+
+
+@pytest.mark.parametrize('dtype,mode', [('f64', 'rollout'), ('f64', 'iterate'), ('f32', 'rollout')])
+def test_box_slow_instances_take_the_interior_point(dtype, mode):
+    """The 12/4 input box's fallback (mpcb_asipm.h): on draws where the active set's backup rule is
+    slow (sine references, +-5 N wind) the instances unconverged after AS_IPM_AFTER passes are
+    solved by the interior point, as in oracle.ocp.pdas_solve.  fp64: the device against the oracle
+    at 1e-9 normwise, same statuses (all OK).  fp32: its interior point stops at mu <= 1e-6 (the
+    17/6 fp32 tolerances), so it is checked against the fp64 oracle at 5e-4 normwise, inside the
+    box."""
+    from test_oracle_ocp import hard_box_inputs
+    from oracle.ocp import AS_IPM_AFTER
+    N, B = 18, 192
+    inp = hard_box_inputs(B, N, 11)
+    m = _mpc(N, dtype, True, B)
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    x0, xref, uref, wind = (cast(inp[k]) for k in ('x0', 'xref', 'uref', 'wind'))
+    spec = OcpSpec(N=N, lbu=np.zeros(4), ubu=np.full(4, 65.0))
+    if mode == 'iterate':
+        rng = np.random.default_rng(3)
+        xbar = cast(xref + rng.normal(scale=0.05, size=(B, N + 1, 12)))
+        ubar = cast(uref + rng.normal(scale=1.0, size=(B, N, 4)))
+        m.solve_iterate(x0, xbar, ubar, xref, uref, wind=wind)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind, mode='iterate', xbar=xbar, ubar=ubar)
+    else:
+        m.solve(x0, xref, uref, wind=wind)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind)
+    u0, X, U, st = _outputs(m)
+    qs = m.qp_stats(B).cpu().numpy()
+    fb = qs[:, 0] > AS_IPM_AFTER
+    e = max(relerr(u0, o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max())
+    print(f'{dtype} {mode}: {fb.sum()} instances took the interior point (oracle {(o["iters"] > AS_IPM_AFTER).sum()}), '
+          f'max rel err {e:.2e}, status {np.bincount(st, minlength=5).tolist()}')
+    assert fb.sum() >= 5
+    assert (st == 0).all() and (o['status'] == 0).all()
+    assert e < (1e-9 if dtype == 'f64' else 5e-4)
+    tb = 1e-7 if dtype == 'f64' else 1e-4   # (interior iterates; fp32: its residual bound 1e-5)
+    assert (U >= -tb).all() and (U <= 65 + tb).all()

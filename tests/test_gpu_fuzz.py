@@ -1,0 +1,92 @@
+"""Randomised GPU parity sweep: seeded random configurations of the 12/4 solve (horizon, batch,
+handle size, precision, input box, rollout / iterate mode, wind, hover or sine references)
+through the C ABI against the oracle on identical inputs (fp32 inputs rounded before the oracle
+sees them).  The handle's max_batch is drawn above the call's batch, so the kernel path (chosen
+at creation from max_batch) and the call's batch vary independently.
+
+Tolerances, normwise per instance: fp64 1e-9 (tests/test_gpu_parity.py).  fp32 5e-5 on u0
+everywhere and on X, U up to N = 40 (the BASELINE horizons); beyond that the fp32 open-loop
+rollout that rollout mode linearises at drifts from the fp64 one, and X, U with it, roughly as N^2
+(measured 6e-5 at N = 56, 1.4e-4 at 80, 3.1e-4 at 105; iterate mode, which takes the iterate as
+given, stays near 1e-5 at N = 108), so the X / U bound is 5e-5 (N / 40)^2 there.  fp32 instances
+that the input box handed to the interior point (mpcb_asipm.h, passes > AS_IPM_AFTER) are held to
+its fp32 accuracy, 5e-4 (tests/test_gpu_edges.py).
+"""
+import numpy as np
+import pytest
+
+from oracle.inputs import make_inputs
+from oracle.ocp import OcpSpec, mpc_solve
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+CASES = 32
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, dtype=np.float64).reshape(b.shape[0], -1)
+    return np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1.0)
+
+
+def draw(case):
+    rng = np.random.default_rng(7000 + case)
+    big = case % 8 == 7   # a large-chunk case now and then (thread-per-instance / chunked paths)
+    box = bool(rng.random() < 0.4) and not big   # (the oracle's active set over 20k instances is slow)
+    return dict(
+        box=box,
+        dtype='f32' if rng.random() < 0.5 else 'f64',
+        N=int(rng.integers(1, 65 if box else 121)) if not big else int(rng.integers(5, 31)),
+        B=int(rng.integers(1, 3000)) if not big else int(rng.integers(16000, 24000)),
+        iterate=bool(rng.random() < 0.35),
+        wind=bool(rng.random() < 0.3),
+        ref='c3' if rng.random() < 0.5 else 'c2',
+        extra=float(rng.random()),
+        seed=int(rng.integers(1 << 30)))
+
+
+@pytest.mark.parametrize('case', range(CASES))
+def test_random_config_matches_oracle(case):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    c = draw(case)
+    N, B, box, dtype = c['N'], c['B'], c['box'], c['dtype']
+    max_batch = B + int(c['extra'] * B)
+    rng = np.random.default_rng(c['seed'])
+    inp = make_inputs(c['ref'], ids=np.arange(B, dtype=np.uint64) + np.uint64(c['seed'] % 100000), N=N)
+    wind = 5.0 * (2.0 * rng.random((B, 3)) - 1.0) if c['wind'] else None
+    cast = (lambda a: None if a is None else a.astype(np.float32).astype(np.float64)) if dtype == 'f32' \
+        else (lambda a: a)
+    x0, xref, uref, wind = cast(inp['x0']), cast(inp['xref']), cast(inp['uref']), cast(wind)
+    spec = OcpSpec(N=N, lbu=np.zeros(4) if box else None, ubu=np.full(4, 65.0) if box else None)
+    m = BatchedMPC(MPCConfig(N=N, dtype=dtype, lbu=spec.lbu, ubu=spec.ubu), max_batch=max_batch)
+    if c['iterate']:
+        xbar = cast(xref + rng.normal(scale=0.05, size=(B, N + 1, 12)))
+        ubar = cast(uref + rng.normal(scale=1.0, size=(B, N, 4)))
+        m.solve_iterate(x0, xbar, ubar, xref, uref, wind=wind)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind, mode='iterate', xbar=xbar, ubar=ubar)
+    else:
+        m.solve(x0, xref, uref, wind=wind)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind)
+    torch.cuda.synchronize()
+    u0 = m.get_control().cpu().numpy()
+    X = m.get_state_trajectory().cpu().numpy()
+    U = m.get_input_trajectory().cpu().numpy()
+    st = m.get_status().cpu().numpy()
+    eu, ex, eU = relerr(u0, o['u0']), relerr(X, o['X']), relerr(U, o['U'])
+    fb = np.zeros(B, dtype=bool)
+    if box:
+        from oracle.ocp import AS_IPM_AFTER
+        fb = m.qp_stats(B).cpu().numpy()[:, 0] > AS_IPM_AFTER
+    print(f'case {case} {c} max_batch={max_batch}: rel err u0 {eu.max():.2e} X {ex.max():.2e} U {eU.max():.2e}, '
+          f'status {np.bincount(st, minlength=5).tolist()} oracle {np.bincount(o["status"], minlength=5).tolist()}, '
+          f'interior-point fallbacks {fb.sum()}')
+    assert (st == o['status']).all()
+    if dtype == 'f64':
+        assert max(eu.max(), ex.max(), eU.max()) < 1e-9
+    else:
+        tu = np.where(fb, 5e-4, 5e-5)
+        txu = np.where(fb, 5e-4, 5e-5 * max(1.0, (N / 40) ** 2))
+        assert (eu < tu).all() and (ex < txu).all() and (eU < txu).all()
+    if box:
+        assert (U >= -1e-6 * 65).all() and (U <= 65 * (1 + 1e-6)).all()

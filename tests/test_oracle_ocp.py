@@ -87,3 +87,29 @@ def test_inputs_reproducible_per_instance():
     assert np.array_equal(a['x0'][5:], b['x0'])
     assert np.array_equal(a['xref'][5:], b['xref'])
     assert CONFIGS['c5']['batch'] == 1048576
+
+
+def hard_box_inputs(B, N, seed):
+    """Input-box draws on which the active set's backup rule is slow: sine references plus a
+    +-5 N wind per instance (tests/test_gpu_edges.py uses the same draws on the device)."""
+    inp = make_inputs('c3', ids=np.arange(B, dtype=np.uint64) + np.uint64(seed), N=N)
+    inp['wind'] = 5.0 * (2.0 * np.random.default_rng(seed).random((B, 3)) - 1.0)
+    return inp
+
+
+def test_pdas_hands_slow_instances_to_the_interior_point():
+    """oracle.ocp.pdas_solve's fallback: instances still unconverged after AS_IPM_AFTER passes are
+    solved by the interior point; they end OK and agree with the independent BVLS solve."""
+    from oracle.ocp import AS_IPM_AFTER
+    N, B = 18, 192
+    inp = hard_box_inputs(B, N, 11)
+    spec = OcpSpec(N=N, lbu=np.zeros(4), ubu=np.full(4, 65.0))
+    o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], spec, wind=inp['wind'], return_lin=True)
+    assert (o['status'] == 0).all()
+    fb = np.nonzero(o['iters'] > AS_IPM_AFTER)[0]
+    assert len(fb) >= 5   # the draw has slow instances
+    sel = fb[:6]
+    du = dense_box_qp(o['A'][sel], o['B'][sel], o['gap'][sel], np.zeros((len(sel), 12)), o['xbar'][sel],
+                      o['ubar'][sel], inp['xref'][sel], inp['uref'][sel], spec)
+    assert np.abs(o['ubar'][sel] + du - o['U'][sel]).max() < 1e-5
+    assert (o['U'] >= -1e-9).all() and (o['U'] <= 65 + 1e-9).all()

@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/r05_b14; mkdir -p $O
+O=gpurun_out/r05_b19; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_edges.py -v -s --timeout 120 --timeout-method thread -k order > $O/edges.log 2>&1
-echo b14_done
+timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -q -s --timeout 150 --timeout-method thread -k "17 or 20 or 24 or 27 or 28 or 10 or 30" > $O/fuzz.log 2>&1 || true
+echo b19_done
