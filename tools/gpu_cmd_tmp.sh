@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/r05_b19; mkdir -p $O
+O=gpurun_out/r05_b21; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -q -s --timeout 150 --timeout-method thread -k "17 or 20 or 24 or 27 or 28 or 10 or 30" > $O/fuzz.log 2>&1 || true
-echo b19_done
+timeout -k 10 400 python tools/box_ipm_direct.py > $O/box_ipm_direct.txt 2>&1
+echo b20_done
