@@ -1,0 +1,110 @@
+"""Randomised GPU parity sweep of the full 17/6 path (the reference's own OCP family): seeded
+random horizon, batch, handle size, boxes (none / input / input + state), rollout or iterate mode,
+per-instance or stage-varying parameters, fp64 or fp32, through the C ABI against the oracle
+(oracle/full.py) on identical inputs.  Bounds: fp64 1e-9 normwise without boxes and 1e-7 with
+them (the interior point and its polish agree with the oracle to ~1e-12 on the fixed tests;
+the margin covers the iterates' rounding on random draws), same statuses.  fp32 against the fp64
+oracle on u0: 5e-4 without boxes and 5e-3 with the input box.  The 6x6 input block (alpha-rate
+weight 1e-5) is ill-conditioned in single precision: tests/test_gpu_full17.py's fixed draws reach
+2.7e-5, but random draws here reached 1.1e-4 unboxed and 2.8e-3 boxed, and stopping the fp32
+interior point at mu <= 1e-7 or 1e-8 instead of 1e-6 changed none of them.  No state box in fp32
+(refused by the library).
+"""
+import numpy as np
+import pytest
+
+from oracle.full import FullSpec, default_p25, mpc_solve17
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+CASES = 16
+LBU17 = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])
+UBU17 = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
+SB_LO = np.array([-1.5, -1.5, 0, -0.174532925, -0.174532925, -0.349066, -1.0, -1.0, -1.0, -0.0872665, -0.0872665,
+                  -0.0872665, -0.174532925, -0.523599, -1.5, -1.5, -2.5])
+SB_HI = np.array([1.5, 1.5, 5.0, 0.174532925, 0.174532925, 0.349066, 1.0, 1.0, 1.0, 0.0872665, 0.0872665,
+                  0.0872665, 1.22173, 0.523599, 1.5, 1.5, 2.5])
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, dtype=np.float64).reshape(b.shape[0], -1)
+    return np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1.0)
+
+
+def draw(case):
+    rng = np.random.default_rng(9100 + case)
+    bounds = ('none', 'input', 'all')[int(rng.integers(3))]
+    dtype = 'f32' if (bounds != 'all' and rng.random() < 0.3) else 'f64'
+    return dict(bounds=bounds, dtype=dtype, N=int(rng.integers(5, 61)), B=int(rng.integers(1, 97)),
+                iterate=bool(rng.random() < 0.35), stage_p=bool(rng.random() < 0.3),
+                extra=int(rng.integers(0, 64)), seed=int(rng.integers(1 << 30)))
+
+
+def inputs(B, N, rng, stage_p):
+    x0 = np.zeros((B, 17))
+    x0[:, 0:3] = rng.uniform(-1, 1, (B, 3))
+    x0[:, 2] += 3.5
+    x0[:, 3:6] = rng.uniform(-0.17, 0.17, (B, 3))
+    x0[:, 6:9] = rng.uniform(-0.5, 0.5, (B, 3))
+    x0[:, 9:12] = rng.uniform(-0.087, 0.087, (B, 3))
+    x0[:, 12:14] = rng.uniform(-0.2, 0.2, (B, 2))
+    x0[:, 14:17] = rng.uniform(-0.3, 0.3, (B, 3))
+    x0 = np.clip(x0, 0.5 * SB_LO, 0.5 * SB_HI)   # (inside the state box's stage-1 reach)
+    x0[:, 2] = 3.5 + rng.uniform(-0.5, 0.5, B)
+    xref = np.zeros((B, N + 1, 17))
+    xref[..., 2] = 3.5
+    xref[..., 14] = 0.2
+    uref = np.zeros((B, N, 6))
+    uref[..., :4] = 22.0725
+    if stage_p:
+        p = np.tile(default_p25(), (B, N, 1))
+        p[..., :24] = rng.uniform(-0.5, 0.5, (B, N, 24))
+    else:
+        p = np.tile(default_p25(), (B, 1))
+        p[:, :24] = rng.uniform(-0.5, 0.5, (B, 24))
+    return x0, xref, uref, p
+
+
+@pytest.mark.parametrize('case', range(CASES))
+def test_random_full17_config_matches_oracle(case):
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    c = draw(case)
+    N, B, dtype = c['N'], c['B'], c['dtype']
+    rng = np.random.default_rng(c['seed'])
+    x0, xref, uref, p = inputs(B, N, rng, c['stage_p'])
+    kw = {}
+    if c['bounds'] in ('input', 'all'):
+        kw.update(lbu=LBU17, ubu=UBU17)
+    if c['bounds'] == 'all':
+        kw.update(lbx=SB_LO, ubx=SB_HI)
+    m = BatchedMPC(MPCConfig.full(N=N, dtype=dtype, **kw), max_batch=B + c['extra'])
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    x0, xref, uref, p = cast(x0), cast(xref), cast(uref), cast(p)
+    m.set_params(p)
+    spec = FullSpec(N=N, **kw)
+    if c['iterate']:
+        xb = cast(x0[:, None, :] + rng.normal(0, 0.03, (B, N + 1, 17)))
+        ub = cast(uref + rng.normal(0, 0.5, (B, N, 6)))
+        m.solve_iterate(x0, xb, ub, xref, uref)
+        o = mpc_solve17(x0, xref, uref, spec, p, mode='iterate', xbar=xb, ubar=ub)
+    else:
+        m.solve(x0, xref, uref)
+        o = mpc_solve17(x0, xref, uref, spec, p)
+    torch.cuda.synchronize()
+    u0 = m.get_control().cpu().numpy()
+    X = m.get_state_trajectory().cpu().numpy()
+    U = m.get_input_trajectory().cpu().numpy()
+    st = m.get_status().cpu().numpy()
+    e = [relerr(u0, o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max()]
+    print(f'case {case} {c}: rel err u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e}, status '
+          f'{np.bincount(st, minlength=5).tolist()} oracle {np.bincount(o["status"], minlength=5).tolist()}')
+    if dtype == 'f64':
+        assert (st == o['status']).all()
+        ok = st == 0
+        assert max(relerr(u0, o['u0'])[ok].max(initial=0), relerr(X, o['X'])[ok].max(initial=0),
+                   relerr(U, o['U'])[ok].max(initial=0)) <= (1e-9 if c['bounds'] == 'none' else 1e-7)
+    else:
+        assert (st == 0).all()
+        assert e[0] <= (5e-4 if c['bounds'] == 'none' else 5e-3)
