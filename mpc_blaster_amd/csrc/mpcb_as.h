@@ -776,7 +776,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     // (never recomputed: its active set is still empty) P2's unconstrained pass
     kc = changed ? WB - 1 - Mk::clz(changed) : -1;
     // the instance is finished: converged, or the pass cap
-    const bool fin_now = write && (gconv || git + 1 >= a.max_as_iter);
+    // (or, with the fallback, the first pass violates more than 7/20 of the horizon's input
+    // components: oracle.ocp.AS_IPM_NV_NUM / _DEN, a strongly constrained QP)
+    const bool crowded = BOX && a.as_fb && git == 0 && nV * AS_IPM_NV_DEN > AS_IPM_NV_NUM * N * NU;
+    const bool fin_now = write && (gconv || git + 1 >= a.max_as_iter || crowded);
     if (stage_out && fin_now) flush_out();
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     ++git;

@@ -127,6 +127,9 @@ constexpr int AB2_REC = 12 * NVAR, ABT2_REC = 12 * ABT2_W, KR2_REC = 4 * KR2_W, 
 // the 12/4 input box: active-set passes before an unconverged instance goes to the interior-point
 // fallback (oracle.ocp.AS_IPM_AFTER; mpcb_asipm.h)
 constexpr int AS_IPM_AFTER = 48;
+// ... or after the first pass when it violates more than 7/20 of the horizon's input components
+// (oracle.ocp.AS_IPM_NV_NUM / _DEN)
+constexpr int AS_IPM_NV_NUM = 7, AS_IPM_NV_DEN = 20;
 
 template <class T>
 struct SplitArgs {

@@ -202,6 +202,13 @@ def riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec,
 # needs at most 24 iterations; on the c4 bench draws the active set needs at most 39 passes, so
 # the fallback never runs there.
 AS_IPM_AFTER, AS_IPM_ITERS = 48, 100
+# ... and an instance whose first pass (the unconstrained solution) violates more than 7/20 of the
+# horizon's input components is handed over at once: on strongly constrained draws (sine
+# references, the iterate perturbed by 0.05 / 1 N, N = 11) 801 of the 803 of 1500 instances that
+# need more than 48 passes violate more than 16 of 44 after the first, and the instances there
+# that the active set does finish need ~19 passes, as many as the interior point's iterations;
+# on the c4 draws no instance violates more than 19 of 120 (tools/box_ipm_direct.py)
+AS_IPM_NV_NUM, AS_IPM_NV_DEN = 7, 20
 
 
 def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int = 3):
@@ -215,10 +222,11 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     element of V with the least index k*nu + m is exchanged (Murty's least-index backup rule,
     finite for a P-matrix LCP).  Measured on 2000 c4 instances: the least index converges in at
     most 28 iterations where the largest index needs up to 132 (mean 3.8 vs 4.0).  Instances not
-    converged after min(max_as_iter, AS_IPM_AFTER) passes are handed to the interior point (see
+    converged after min(max_as_iter, AS_IPM_AFTER) passes, or whose first pass violates more than
+    AS_IPM_NV_NUM / AS_IPM_NV_DEN of the input components, are handed to the interior point (see
     AS_IPM_AFTER); their status and solution are the interior point's, their iteration count the
     passes plus its iterations.
-    Returns dx, du, status, iterations.
+    Returns dx, du, status, iterations, the mask of the instances handed over.
     """
     Bsz, N = xbar.shape[0], spec.N
     NX, NU = A.shape[-1], Bm.shape[-1]
@@ -234,12 +242,13 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
     out_dx = np.zeros((Bsz, N + 1, NX))
     out_du = np.zeros((Bsz, N, NU))
     flat_idx = np.arange(N * NU).reshape(N, NU)
+    stopped = np.zeros(Bsz, dtype=bool)   # converged, or handed over after the first pass
     for it in range(min(spec.max_as_iter, AS_IPM_AFTER)):
         fixed = low | up
         delta = np.where(low, lb - ubar, np.where(up, ub - ubar, 0.0))
         dx, du, mu, ok2 = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec, fixed, delta)
-        act = ~done
-        ok &= ok2 | done
+        act = ~stopped
+        ok &= ok2 | stopped
         out_dx[act], out_du[act] = dx[act], du[act]
         iters[act] += 1
         u = ubar + du
@@ -250,8 +259,11 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
         V = v_lo | v_hi | v_fl | v_fu
         nV = V.sum(axis=(1, 2))
         conv = nV == 0
-        done |= conv
-        if done.all():
+        done |= conv & ~stopped
+        if it == 0:
+            stopped |= nV * AS_IPM_NV_DEN > AS_IPM_NV_NUM * N * NU
+        stopped |= done
+        if stopped.all():
             break
         full = (nV < best) | (pcount > 0)
         improve = nV < best
@@ -260,7 +272,7 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
         # backup: only the least-index infeasible element
         first = np.where(V, flat_idx[None], N * NU).reshape(Bsz, -1).min(axis=1)
         sel = np.where(full[:, None, None], V, flat_idx[None] == first[:, None, None])
-        sel &= ~done[:, None, None]
+        sel &= ~stopped[:, None, None]
         low = np.where(sel & v_lo, True, np.where(sel & v_fl, False, low))
         up = np.where(sel & v_hi, True, np.where(sel & v_fu, False, up))
     status = np.where(done, STATUS_OK, STATUS_MAXITER).astype(np.int32)
@@ -273,7 +285,9 @@ def pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec, pbar: int
                                                sub(uref), spec, max_iter=AS_IPM_ITERS, centring='adaptive')
         out_dx[fb], out_du[fb], status[fb] = fdx, fdu, fst
         iters[fb] += fit
-    return out_dx, out_du, status, iters
+    handed = np.zeros(Bsz, dtype=bool)
+    handed[fb] = True
+    return out_dx, out_du, status, iters, handed
 
 
 # IPM_BREAK_TOL: a Newton system that loses positive definiteness, or a collapsed step, once mu is
@@ -770,16 +784,18 @@ def mpc_solve(x0, xref, uref, spec: OcpSpec, wind=None, mode='rollout', xbar=Non
     A, Bm, gap = linearise(xbar, ubar, spec, wind)
     dx0 = x0 - xbar[:, 0]
     if spec.boxed:
-        dx, du, status, iters = pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
+        dx, du, status, iters, handed = pdas_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
     else:
         dx, du, _, ok = riccati_solve(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec)
         status = np.where(ok, STATUS_OK, STATUS_QP_FAIL).astype(np.int32)
         iters = np.zeros(Bsz, dtype=np.int32)
+        handed = np.zeros(Bsz, dtype=bool)
     X = xbar + dx
     U = ubar + du
     bad = ~(np.isfinite(X).all(axis=(1, 2)) & np.isfinite(U).all(axis=(1, 2)))
     status = np.where(bad, STATUS_NAN, status).astype(np.int32)
-    out = dict(u0=U[:, 0].copy(), X=X, U=U, status=status, iters=iters, xbar=xbar, ubar=ubar)
+    # (fallback: the instances the input box's active set handed to the interior point)
+    out = dict(u0=U[:, 0].copy(), X=X, U=U, status=status, iters=iters, xbar=xbar, ubar=ubar, fallback=handed)
     if return_lin:
         out.update(A=A, B=Bm, gap=gap)
     return out
