@@ -225,7 +225,9 @@ int mpcb_poc_jacobians(int64_t B, const double* pose, double stream_velocity, co
  * Work statistics of the last solve on an input-box handle.  12/4 (the active-set QP, c4): per
  * instance ``out[2b]`` = forward passes until its active set was the KKT point (including the
  * first, after the unconstrained Riccati pass) and ``out[2b+1]`` = backward stages its masked
- * Riccati passes recomputed (restarts skip the stages above the highest changed one).  17/6 (the
+ * Riccati passes recomputed (restarts skip the stages above the highest changed one); an instance
+ * the active set handed to the interior point (mpcb_config.max_as_iter) adds its iterations to
+ * ``out[2b]`` and N per iteration to ``out[2b+1]``.  17/6 (the
  * interior point): ``out[2b]`` = interior-point iterations (Newton directions computed),
  * ``out[2b+1]`` = polish passes (fp64 state box).  ``out`` is a DEVICE int32 array [B, 2], B <= that
  * solve's batch.  Reference counterpart: HPIPM's ``get_stats('qp_iter')``.  MPCB_E_UNSUPPORTED on
