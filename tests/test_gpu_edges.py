@@ -201,3 +201,22 @@ def test_box_slow_instances_take_the_interior_point(dtype, mode):
     assert e < (1e-9 if dtype == 'f64' else 5e-4)
     tb = 1e-7 if dtype == 'f64' else 1e-4   # (interior iterates; fp32: its residual bound 1e-5)
     assert (U >= -tb).all() and (U <= 65 + tb).all()
+
+
+def test_box_interior_point_from_start_matches_oracle():
+    """max_as_iter = 1: every instance whose unconstrained solution leaves the box goes straight to
+    the interior point (mpcb.h max_as_iter), on the device as in oracle.ocp.pdas_solve."""
+    from mpc_blaster_amd import BatchedMPC, MPCConfig
+    from test_oracle_ocp import hard_box_inputs
+    N, B = 18, 192
+    inp = hard_box_inputs(B, N, 12)
+    m = BatchedMPC(MPCConfig(N=N, dtype='f64', lbu=np.zeros(4), ubu=np.full(4, 65.0), max_as_iter=1), max_batch=B)
+    m.solve(inp['x0'], inp['xref'], inp['uref'], wind=inp['wind'])
+    u0, X, U, st = _outputs(m)
+    spec = OcpSpec(N=N, lbu=np.zeros(4), ubu=np.full(4, 65.0), max_as_iter=1)
+    o = mpc_solve(inp['x0'], inp['xref'], inp['uref'], spec, wind=inp['wind'])
+    e = max(relerr(u0, o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max())
+    print(f'interior point from the start: {o["fallback"].sum()} of {B} handed over, max rel err {e:.2e}')
+    assert o['fallback'].sum() > B // 2
+    assert (st == 0).all() and (o['status'] == 0).all()
+    assert e < 1e-9
