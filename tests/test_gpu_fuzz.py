@@ -43,13 +43,23 @@ def draw(case):
         wind=bool(rng.random() < 0.3),
         ref='c3' if rng.random() < 0.5 else 'c2',
         extra=float(rng.random()),
-        seed=int(rng.integers(1 << 30)))
+        seed=int(rng.integers(1 << 30)),
+        # (drawn last so the earlier draws keep their values) the library's opt-in paths, for the
+        # unconstrained problem: the single-kernel solver, the small-chunk path, P1 and P2 as two
+        # launches, the captured-scalar P2 instead of the tangent export
+        path=(None if box else [None, None, 'single', 'small', 'two', 'notan'][int(rng.integers(6))]))
+
+
+PATH_ENV = {'single': {'MPCB_SPLIT_MIN_BATCH': str(1 << 40)}, 'small': {'MPCB_SMALL_MAX': '1000000'},
+            'two': {'MPCB_FUSE_P12': '0'}, 'notan': {'MPCB_P1_TAN': '0'}}
 
 
 @pytest.mark.parametrize('case', range(CASES))
-def test_random_config_matches_oracle(case):
+def test_random_config_matches_oracle(case, monkeypatch):
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     c = draw(case)
+    for k, v in PATH_ENV.get(c['path'], {}).items():
+        monkeypatch.setenv(k, v)
     N, B, box, dtype = c['N'], c['B'], c['box'], c['dtype']
     max_batch = B + int(c['extra'] * B)
     rng = np.random.default_rng(c['seed'])
