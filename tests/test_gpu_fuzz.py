@@ -13,6 +13,8 @@ bound is 1e-4 (N / 40)^2 there.  fp32 instances
 that the input box hands to the interior point (mpcb_asipm.h; the oracle's ``fallback`` mask) are
 held to its fp32 accuracy, 5e-4 (tests/test_gpu_edges.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -22,7 +24,7 @@ from oracle.ocp import OcpSpec, mpc_solve
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-CASES = 32
+CASES = int(os.environ.get('MPCB_FUZZ_CASES', 32))   # (a deeper sweep on demand)
 
 
 def relerr(a, b):

@@ -10,6 +10,8 @@ weight 1e-5) is ill-conditioned in single precision: tests/test_gpu_full17.py's 
 interior point at mu <= 1e-7 or 1e-8 instead of 1e-6 changed none of them.  No state box in fp32
 (refused by the library).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -18,7 +20,7 @@ from oracle.full import FullSpec, default_p25, mpc_solve17
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-CASES = 16
+CASES = int(os.environ.get('MPCB_FUZZ_CASES', 16))   # (a deeper sweep on demand)
 LBU17 = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])
 UBU17 = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
 SB_LO = np.array([-1.5, -1.5, 0, -0.174532925, -0.174532925, -0.349066, -1.0, -1.0, -1.0, -0.0872665, -0.0872665,
