@@ -10,8 +10,11 @@ rollout that rollout mode linearises at drifts from the fp64 one, and X, U with 
 (measured 6e-5 at N = 56, 1.4e-4 at 80, 3.1e-4 at 105; iterate mode, which takes the iterate as
 given, stays near 1e-5 at N = 108; the small-chunk path reached 2.6e-4 at N = 89), so the X / U
 bound is 1e-4 (N / 40)^2 there.  fp32 instances
-that the input box hands to the interior point (mpcb_asipm.h; the oracle's ``fallback`` mask) are
-held to its fp32 accuracy, 5e-4 (tests/test_gpu_edges.py).
+fp32 box cases are held to optimality instead of to the fp64 minimiser: the QP objective of the
+device's U (states by the oracle's linearised dynamics) within 1e-5 of the oracle's optimum, u0
+within 5e-3.  Along nearly flat directions of strongly constrained QPs the fp32 active set and the
+fp32 interior point alike land up to ~4e-3 off the minimiser at an objective within ~1e-6 (the
+128-case sweep, profiles/r05/gpu_fuzz_b29_128.log).
 """
 import os
 
@@ -53,6 +56,23 @@ def draw(case):
         path=(None if box else [None, None, 'single', 'small', 'two', 'notan'][int(rng.integers(6))]))
 
 
+def qp_objective(o, U, x0, xref, uref, spec):
+    """The SQP_RTI step's QP objective at input trajectory U (clipped into the box), states by the
+    linearised dynamics of the oracle's linearisation (o: mpc_solve(..., return_lin=True))."""
+    A, Bm, gap, xbar, ubar = o['A'], o['B'], o['gap'], o['xbar'], o['ubar']
+    B, N = U.shape[0], spec.N
+    U = np.clip(np.asarray(U, dtype=np.float64), spec.lbu, spec.ubu)
+    du = U - ubar
+    dx = np.empty((B, N + 1, 12))
+    dx[:, 0] = x0 - xbar[:, 0]
+    for k in range(N):
+        dx[:, k + 1] = np.einsum('bij,bj->bi', A[:, k], dx[:, k]) + np.einsum('bij,bj->bi', Bm[:, k], du[:, k]) + gap[:, k]
+    ex = xbar + dx - np.broadcast_to(xref, (B, N + 1, 12))
+    eu = U - np.broadcast_to(uref, (B, N, 4))
+    J = spec.s * (np.einsum('bki,ij,bkj->b', ex[:, :N], spec.Q, ex[:, :N]) + np.einsum('bki,ij,bkj->b', eu, spec.R, eu))
+    return J + np.einsum('bi,ij,bj->b', ex[:, N], spec.QN, ex[:, N])
+
+
 PATH_ENV = {'single': {'MPCB_SPLIT_MIN_BATCH': str(1 << 40)}, 'small': {'MPCB_SMALL_MAX': '1000000'},
             'two': {'MPCB_FUSE_P12': '0'}, 'notan': {'MPCB_P1_TAN': '0'}}
 
@@ -77,10 +97,10 @@ def test_random_config_matches_oracle(case, monkeypatch):
         xbar = cast(xref + rng.normal(scale=0.05, size=(B, N + 1, 12)))
         ubar = cast(uref + rng.normal(scale=1.0, size=(B, N, 4)))
         m.solve_iterate(x0, xbar, ubar, xref, uref, wind=wind)
-        o = mpc_solve(x0, xref, uref, spec, wind=wind, mode='iterate', xbar=xbar, ubar=ubar)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind, mode='iterate', xbar=xbar, ubar=ubar, return_lin=True)
     else:
         m.solve(x0, xref, uref, wind=wind)
-        o = mpc_solve(x0, xref, uref, spec, wind=wind)
+        o = mpc_solve(x0, xref, uref, spec, wind=wind, return_lin=True)
     torch.cuda.synchronize()
     u0 = m.get_control().cpu().numpy()
     X = m.get_state_trajectory().cpu().numpy()
@@ -94,9 +114,15 @@ def test_random_config_matches_oracle(case, monkeypatch):
     assert (st == o['status']).all()
     if dtype == 'f64':
         assert max(eu.max(), ex.max(), eU.max()) < 1e-9
+    elif not box:
+        txu = 5e-5 if N <= 40 else 1e-4 * (N / 40) ** 2
+        assert (eu < 5e-5).all() and (ex < txu).all() and (eU < txu).all()
     else:
-        tu = np.where(fb, 5e-4, 5e-5)
-        txu = np.where(fb, 5e-4, 5e-5 if N <= 40 else 1e-4 * (N / 40) ** 2)
-        assert (eu < tu).all() and (ex < txu).all() and (eU < txu).all()
+        # fp32 box QPs: held to optimality, not to the fp64 minimiser -- along nearly flat
+        # directions of strongly constrained QPs fp32 lands up to ~4e-3 off the minimiser with
+        # the objective within ~1e-6 of the optimum
+        gap = qp_objective(o, U, x0, xref, uref, spec) / np.abs(qp_objective(o, o['U'], x0, xref, uref, spec)) - 1.0
+        print(f'  fp32 box: objective gap max {gap.max():.2e}, u0 {eu.max():.2e}')
+        assert (gap < 1e-5).all() and (eu < 5e-3).all()
     if box:
         assert (U >= -1e-6 * 65).all() and (U <= 65 * (1 + 1e-6)).all()
