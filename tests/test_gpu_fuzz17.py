@@ -1,14 +1,15 @@
 """Randomised GPU parity sweep of the full 17/6 path (the reference's own OCP family): seeded
 random horizon, batch, handle size, boxes (none / input / input + state), rollout or iterate mode,
 per-instance or stage-varying parameters, fp64 or fp32, through the C ABI against the oracle
-(oracle/full.py) on identical inputs.  Bounds: fp64 1e-9 normwise without boxes and 1e-7 with
-them (the interior point and its polish agree with the oracle to ~1e-12 on the fixed tests;
-the margin covers the iterates' rounding on random draws), same statuses.  fp32 against the fp64
-oracle on u0: 5e-4 without boxes and 5e-3 with the input box.  The 6x6 input block (alpha-rate
-weight 1e-5) is ill-conditioned in single precision: tests/test_gpu_full17.py's fixed draws reach
-2.7e-5, but random draws here reached 1.1e-4 unboxed and 2.8e-3 boxed, and stopping the fp32
-interior point at mu <= 1e-7 or 1e-8 instead of 1e-6 changed none of them.  No state box in fp32
-(refused by the library).
+(oracle/full.py) on identical inputs.  Unboxed: fp64 1e-9 normwise, fp32 u0 5e-4 against the
+fp64 oracle.  Boxed QPs are held to optimality, since along nearly flat directions the minimiser
+is ill-determined (a 64-case sweep: an fp64 state-box instance 6.4e-7 off the oracle's minimiser
+at an objective 2.4e-14 from it; fp32 input-box u0 up to 8.9e-3 off at objectives within 1.6e-6;
+the 6x6 input block with its alpha-rate weight 1e-5 is ill-conditioned, and a tighter fp32
+interior-point stop changed nothing): the QP objective of the device's U (states by the oracle's
+linearised dynamics) within 1e-10 (fp64) / 1e-5 (fp32) of the oracle's, fp64 state rows within
+1e-9 of the box, same statuses, and the minimiser within 1e-5 (fp64) / u0 within 2e-2 (fp32).
+No state box in fp32 (refused by the library).
 """
 import os
 
@@ -69,6 +70,32 @@ def inputs(B, N, rng, stage_p):
     return x0, xref, uref, p
 
 
+def qp_objective(o, U, x0, xref, uref, spec):
+    """The step's QP objective at input trajectory U (clipped into the input box), states by the
+    oracle's linearised dynamics (o: mpc_solve17's A, B, gap, xbar, ubar); also the largest
+    state-box violation of those states (0 without a state box)."""
+    A, Bm, gap, xbar, ubar = o['A'], o['B'], o['gap'], o['xbar'], o['ubar']
+    B, N = U.shape[0], spec.N
+    U = np.asarray(U, dtype=np.float64)
+    if spec.lbu is not None:
+        U = np.clip(U, spec.lbu, spec.ubu)
+    du = U - ubar
+    dx = np.empty((B, N + 1, 17))
+    dx[:, 0] = x0 - xbar[:, 0]
+    for k in range(N):
+        dx[:, k + 1] = np.einsum('bij,bj->bi', A[:, k], dx[:, k]) + np.einsum('bij,bj->bi', Bm[:, k], du[:, k]) + gap[:, k]
+    X = xbar + dx
+    ex = X - np.broadcast_to(xref, (B, N + 1, 17))
+    eu = U - np.broadcast_to(uref, (B, N, 6))
+    J = spec.s * (np.einsum('bki,ij,bkj->b', ex[:, :N], spec.Q, ex[:, :N]) + np.einsum('bki,ij,bkj->b', eu, spec.R, eu))
+    J = J + np.einsum('bi,ij,bj->b', ex[:, N], spec.QN, ex[:, N])
+    viol = np.zeros(B)
+    if spec.lbx is not None:
+        Xs = X[:, 1:N]
+        viol = np.maximum(np.maximum(spec.lbx - Xs, Xs - spec.ubx), 0).max(axis=(1, 2))
+    return J, viol
+
+
 @pytest.mark.parametrize('case', range(CASES))
 def test_random_full17_config_matches_oracle(case):
     from mpc_blaster_amd import BatchedMPC, MPCConfig
@@ -102,11 +129,24 @@ def test_random_full17_config_matches_oracle(case):
     e = [relerr(u0, o['u0']).max(), relerr(X, o['X']).max(), relerr(U, o['U']).max()]
     print(f'case {case} {c}: rel err u0 {e[0]:.2e} X {e[1]:.2e} U {e[2]:.2e}, status '
           f'{np.bincount(st, minlength=5).tolist()} oracle {np.bincount(o["status"], minlength=5).tolist()}')
+    ok = (st == 0) & (o['status'] == 0)
+    if c['bounds'] != 'none':
+        Jd, vd = qp_objective(o, U, x0, xref, uref, spec)
+        Jo, vo = qp_objective(o, o['U'], x0, xref, uref, spec)
+        jgap = Jd / np.abs(Jo) - 1.0
+        print(f'  objective gap max {jgap[ok].max(initial=0):.2e}, state-box violation device '
+              f'{vd[ok].max(initial=0):.1e} oracle {vo[ok].max(initial=0):.1e}')
+    emax = max(relerr(u0, o['u0'])[ok].max(initial=0), relerr(X, o['X'])[ok].max(initial=0),
+               relerr(U, o['U'])[ok].max(initial=0))
     if dtype == 'f64':
         assert (st == o['status']).all()
-        ok = st == 0
-        assert max(relerr(u0, o['u0'])[ok].max(initial=0), relerr(X, o['X'])[ok].max(initial=0),
-                   relerr(U, o['U'])[ok].max(initial=0)) <= (1e-9 if c['bounds'] == 'none' else 1e-7)
+        if c['bounds'] == 'none':
+            assert emax <= 1e-9
+        else:   # optimal and feasible as the oracle's; the minimiser itself within 1e-5
+            assert jgap[ok].max(initial=0) <= 1e-10 and vd[ok].max(initial=0) <= 1e-9 and emax <= 1e-5
     else:
         assert (st == 0).all()
-        assert e[0] <= (5e-4 if c['bounds'] == 'none' else 5e-3)
+        if c['bounds'] == 'none':
+            assert e[0] <= 5e-4
+        else:
+            assert jgap.max() <= 1e-5 and e[0] <= 2e-2
