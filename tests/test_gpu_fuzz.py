@@ -27,7 +27,8 @@ from oracle.ocp import OcpSpec, mpc_solve
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-CASES = int(os.environ.get('MPCB_FUZZ_CASES', 32))   # (a deeper sweep on demand)
+CASES = int(os.environ.get('MPCB_FUZZ_CASES', 32))   # (a deeper sweep on demand, from case
+FIRST = int(os.environ.get('MPCB_FUZZ_FIRST', 0))          # MPCB_FUZZ_FIRST on)
 
 
 def relerr(a, b):
@@ -77,7 +78,7 @@ PATH_ENV = {'single': {'MPCB_SPLIT_MIN_BATCH': str(1 << 40)}, 'small': {'MPCB_SM
             'two': {'MPCB_FUSE_P12': '0'}, 'notan': {'MPCB_P1_TAN': '0'}}
 
 
-@pytest.mark.parametrize('case', range(CASES))
+@pytest.mark.parametrize('case', range(FIRST, FIRST + CASES))
 def test_random_config_matches_oracle(case, monkeypatch):
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     c = draw(case)

@@ -21,7 +21,8 @@ from oracle.full import FullSpec, default_p25, mpc_solve17
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
-CASES = int(os.environ.get('MPCB_FUZZ_CASES', 16))   # (a deeper sweep on demand)
+CASES = int(os.environ.get('MPCB_FUZZ_CASES', 16))   # (a deeper sweep on demand, from case
+FIRST = int(os.environ.get('MPCB_FUZZ_FIRST', 0))          # MPCB_FUZZ_FIRST on)
 LBU17 = np.array([0.0, 0.0, 0.0, 0.0, -0.0872665, -0.0872665])
 UBU17 = np.array([65.0, 65.0, 65.0, 65.0, 0.0872665, 0.0872665])
 SB_LO = np.array([-1.5, -1.5, 0, -0.174532925, -0.174532925, -0.349066, -1.0, -1.0, -1.0, -0.0872665, -0.0872665,
@@ -96,7 +97,7 @@ def qp_objective(o, U, x0, xref, uref, spec):
     return J, viol
 
 
-@pytest.mark.parametrize('case', range(CASES))
+@pytest.mark.parametrize('case', range(FIRST, FIRST + CASES))
 def test_random_full17_config_matches_oracle(case):
     from mpc_blaster_amd import BatchedMPC, MPCConfig
     c = draw(case)
