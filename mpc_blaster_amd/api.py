@@ -9,6 +9,7 @@ that stream is synchronised (``torch.cuda.synchronize()`` or reading them on the
 from __future__ import annotations
 
 import ctypes
+import math
 
 import numpy as np
 
@@ -31,6 +32,7 @@ class BatchedMPC:
         self.lib = _lib.load()
         self.cfg = config
         self.device = torch.cuda.current_device() if device is None else int(device)
+        self._tdev = torch.device('cuda', self.device)
         self.max_batch = int(max_batch)
         self._c = config.to_c()
         h = ctypes.c_void_p()
@@ -90,14 +92,14 @@ class BatchedMPC:
         torch = _torch()
         if isinstance(t, np.ndarray) and not t.flags.writeable:
             t = t.copy()   # torch.as_tensor warns on read-only arrays
-        t = torch.as_tensor(t, dtype=self.dtype, device=f'cuda:{self.device}')
+        t = torch.as_tensor(t, dtype=self.dtype, device=self._tdev)
         if t.dim() == len(shape_tail):
             t = t.unsqueeze(0)
         if tuple(t.shape[1:]) != tuple(shape_tail):
             raise ValueError(f'{name}: expected shape [B, {", ".join(map(str, shape_tail))}], '
                              f'got {tuple(t.shape)}')
         t = t.contiguous()
-        n = int(np.prod(shape_tail))
+        n = math.prod(shape_tail)
         if batch is not None and t.shape[0] != batch:
             if allow_broadcast and t.shape[0] == 1:
                 return t, 0
@@ -109,7 +111,7 @@ class BatchedMPC:
 
     def _outputs(self, B, want_traj):
         torch = _torch()
-        dev = f'cuda:{self.device}'
+        dev = self._tdev
         N = self.cfg.N
         self._u0 = torch.empty((B, self.nu), dtype=self.dtype, device=dev)
         self._status = torch.empty((B,), dtype=torch.int32, device=dev)
@@ -187,7 +189,7 @@ class BatchedMPC:
         N = self.cfg.N
         if isinstance(p, np.ndarray) and not p.flags.writeable:
             p = p.copy()   # torch.as_tensor warns on read-only arrays
-        t = torch.as_tensor(p, dtype=self.dtype, device=f'cuda:{self.device}')
+        t = torch.as_tensor(p, dtype=self.dtype, device=self._tdev)
         if t.dim() == 1:
             t = t.reshape(1, 1, -1)
         elif t.dim() == 2:
@@ -216,7 +218,7 @@ class BatchedMPC:
         iterations, polish passes)."""
         torch = _torch()
         B = self._u0.shape[0] if B is None else int(B)
-        out = torch.empty((B, 2), dtype=torch.int32, device=f'cuda:{self.device}')
+        out = torch.empty((B, 2), dtype=torch.int32, device=self._tdev)
         _lib.check(self.lib.mpcb_qp_stats(self._h, B, self._ptr(out), self._stream()))
         return out
 
@@ -248,7 +250,7 @@ class BatchedMPC:
         B = xb.shape[0]
         ub, _ = self._dev(ubar, (N, self.nu), 'ubar', B)
         wd, wd_sb = (None, 0) if wind is None else self._dev(wind, (3,), 'wind', B, allow_broadcast=True)
-        dev = f'cuda:{self.device}'
+        dev = self._tdev
         A = torch.empty((B, N, self.nx, self.nx), dtype=self.dtype, device=dev)
         Bm = torch.empty((B, N, self.nx, self.nu), dtype=self.dtype, device=dev)
         xn = torch.empty((B, N, self.nx), dtype=self.dtype, device=dev)
@@ -276,7 +278,7 @@ class BatchedMPC:
         """Synthetic inputs on device (SURVEY §8 d): x0 [B,12], x_ref, u_ref (broadcast for hover)."""
         torch = _torch()
         N = self.cfg.N
-        dev = f'cuda:{self.device}'
+        dev = self._tdev
         x0 = torch.empty((B, self.nx), dtype=self.dtype, device=dev)
         if ref == 'sine':
             xr = torch.empty((B, N + 1, self.nx), dtype=self.dtype, device=dev)
@@ -296,7 +298,7 @@ class BatchedMPC:
         torch = _torch()
         u, _ = self._dev(u0, (self.nu,), 'u0')
         if counts is None:
-            counts = torch.zeros((self.nu, nbins), dtype=torch.int64, device=f'cuda:{self.device}')
+            counts = torch.zeros((self.nu, nbins), dtype=torch.int64, device=self._tdev)
         _lib.check(self.lib.mpcb_histogram(self._h, u.shape[0], self._ptr(u), float(lo), float(hi),
                                            int(nbins), self._ptr(counts), self._stream()))
         return counts
