@@ -36,6 +36,9 @@
 namespace mpcb {
 namespace asq {
 
+#if defined(MPCB_REF_TRACE) && defined(MPCB_AS_OWNER)
+__device__ int g_ref_trace[128][20];
+#endif
 #ifdef MPCB_AS_STAMPS
 // Diagnostic build only: per-region s_memtime cycles of workgroup 0, wave-summed over the whole
 // kernel ([0] backward init, [1..3] backward stage parts, [4..6] forward stage parts, [7] forward
@@ -94,6 +97,10 @@ __device__ __forceinline__ void dot16abs(float (&acc)[4], float z, const float (
 __device__ __forceinline__ void dot16abs(double (&acc)[4], double z, const double (&r)[16]) {
   asm("s_nop 4\n\t" ASQ_DOT16(ASQ_A, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN16(z, r));
 }
+// acc[*] += sum_{l<12} |bcast_l(z) * r[l]|
+__device__ __forceinline__ void dot12abs(double (&acc)[4], double z, const double (&r)[12]) {
+  asm("s_nop 4\n\t" ASQ_DOT12(ASQ_A, "v_fmac_f64_dpp") : ASQ_OUT4(acc) : ASQ_IN12(z, r));
+}
 // acc[i] += bcast_i(a) * b, i < 12 (lane i's a feeds accumulator i); the fp64 form is
 // mpcb_split.h fmac12_diag
 #define ASQ_D(d, l) "v_fmac_f32_dpp %" #d ", %12, %13 row_newbcast:" #l " row_mask:0xf bank_mask:0xf\n\t"
@@ -149,6 +156,11 @@ template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int6
 // waited for the write acknowledgements of the previous stages' scattered 4/8-B output stores.
 constexpr int OUT_NMAX = 64;   // longer horizons store directly
 template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
+// the box kernel's block per instance: the staged rows, then (fp32) the refinement's N x NU
+// feedforward terms
+template <class T> __host__ __device__ constexpr int box_elems(int N) {
+  return out_elems<T>(N) + (sizeof(T) == 4 ? N * NU : 0);
+}
 
 // Stage masks (active sets, violations: bit k = stage k) of a horizon N <= 32 in 32-bit registers
 // (W32: half the VALU of every mask shift / or in the stage loops), else 64-bit.
@@ -188,7 +200,315 @@ template <class P> __device__ __forceinline__ P* vglobal(P* p) {
   return (P*)(__attribute__((address_space(1))) P*)v;
 }
 
-template <class T, bool BOX, bool W32 = false, bool ITER = false>
+// The fp32 box kernel's refinement + KKT verification of one set (as_body, below, says what and
+// why).  Every lane of the wave runs it (wave-uniform: the DPP blocks need whole rows); groups
+// with ver = false compute along and write nothing.  Its stage loops are latency chains over a
+// few hundred instances, so each keeps its next stage's loads in flight (two register slots, the
+// loop unrolled by two, as the active-set kernel's backward pass).
+// refinement steps per pass before the verification, the refined passes whose multiplier verdicts
+// count, and the verification's tolerance on a multiplier relative to its terms' sum
+constexpr int REF_STEPS = 1, REF_PASSES = 3;
+constexpr double REF_TOL = 0x1p-18;
+template <bool W32> struct RefIn {
+  using M = typename Masks<W32>::M;
+  using T = float;
+  const T* x0;   // this instance's x0
+  Arr<T> XU, GP, ABT, KR, PS;
+  const T* cbase; int64_t cstride;   // the lane's [A|B] column (ABT2 rows or W.ctab)
+  const T* refp; int64_t refs;       // the lane's reference component
+  const T* xrN;
+  const T* QN;
+  const T* SW;                       // s blkdiag(Q, R) (LDS)
+  T* PX;                             // the group's P block (LDS)
+  T* xs; T* us; T* dks;              // the group's staged X rows, U rows, refinement feedforward (LDS)
+  T crow[6];
+  M lowm, upm;
+  T lbm, ubm, tol_u;
+  int N;
+  bool iterate, ver;
+};
+template <bool W32> struct RefOut { typename Masks<W32>::M rd, alo, ahi; };
+
+// run body(k, slot) for k = k0, k0 + dir, ... (N stages) with load(k, slot) one stage ahead in two
+// register slots (every slot a fixed register set; loads for stages outside [0, N) are clamped)
+template <class S, class L, class B>
+__device__ __forceinline__ void ring2(int N, bool down, L&& load, B&& body) {
+  S s0, s1;
+  const int k0 = down ? N - 1 : 0, dir = down ? -1 : 1;
+  auto kc = [&](int k) { return k < 0 ? 0 : (k >= N ? N - 1 : k); };
+  load(k0, s0);
+  for (int i = 0; i < N; i += 2) {
+    const int k = k0 + dir * i;
+    load(kc(k + dir), s1);
+    body(k, s0);
+    if (i + 1 >= N) break;
+    load(kc(k + 2 * dir), s0);
+    body(k + dir, s1);
+  }
+}
+
+template <bool W32>
+__device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
+  using T = float;
+  using Mk = Masks<W32>;
+  using M = typename Mk::M;
+  const int lane = threadIdx.x;
+  const int j = lane & 15;
+  const int jx = j < NX ? j : 0;
+  const int ju = j >= NX ? j - NX : 0;
+  const bool stl = j < NX;
+  const uint64_t mst = lane_mask(stl);
+  const int N = in.N;
+  const bool iterate = in.iterate, ver = in.ver;
+  const Arr<T> XU = in.XU, GP = in.GP, ABT = in.ABT, KR = in.KR, PS = in.PS;
+  const T* const cbase = in.cbase;
+  const int64_t cstride = in.cstride;
+  const T* const refp = in.refp;
+  const int64_t refs = in.refs;
+  const T* const SW = in.SW;
+  T* const PX = in.PX;
+  T* const xs = in.xs;
+  T* const us = in.us;
+  T* const dks = in.dks;
+  const M lowm = in.lowm, upm = in.upm;
+  T crow[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) crow[i] = in.crow[i];
+  // the lane's row of [A|B] (state lanes: variable columns loaded, constant ones crow), fp64
+  auto arow = [&](const T* rv, double (&row)[NZ]) {
+#pragma unroll
+    for (int t = 0; t < NVAR; ++t) row[var_col(t)] = (double)rv[t];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      row[p] = (double)crow[p];
+      row[6 + p] = (double)crow[3 + p];
+    }
+  };
+  M rd = 0, alo = 0, ahi = 0;   // input lanes: released stages, free components beyond a bound
+
+  // (1) the states re-simulated in fp64 from the staged U, x_k into xs
+  struct SF { T rv[NVAR]; T yb, gp; };
+  {
+    double zd = 0.0;   // state lanes dx_i, input lanes du_m
+    if (iterate && stl) zd = (double)in.x0[jx] - (double)XU.at(0)[jx * SS];
+    ring2<SF>(N, false,
+        [&](int k, SF& s) {
+          ldv<T, NVAR, 8>(ABT.at(k) + jx * ABT2_W, s.rv);
+          s.yb = XU.at(k)[j * SS];
+          s.gp = iterate ? GP.at(k)[jx * SS] : T(0);
+        },
+        [&](int k, const SF& s) {
+          double row[NZ];
+          arow(s.rv, row);
+          if (!stl) zd = (double)us[k * NU + ju] - (double)s.yb;
+          else if (ver) xs[k * NX + jx] = (T)((double)s.yb + zd);
+          double acc[4] = {(double)s.gp, 0.0, 0.0, 0.0};
+          dot16(acc, zd, row);
+          if (stl) zd = sum4(acc);
+        });
+    if (stl && ver) xs[N * NX + jx] = (T)((double)XU.at(N)[jx * SS] + zd);
+  }
+  struct SA { T cr[NX]; T rf; };
+  for (int r = 0; r <= REF_STEPS; ++r) {
+    // (2) the adjoint sweep (fp64): lambda_N = QN e_N, g_k = [A|B]_k^T lambda_{k+1} + s blkdiag(Q,
+    // R)(e_k, u_k - uref_k); r < REF_STEPS keeps the input lanes' g_k for the correction (dks),
+    // r = REF_STEPS decides
+    double lam;
+    {
+      const double eN = stl ? (double)xs[N * NX + jx] - (double)in.xrN[jx] : 0.0;
+      double qn[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) qn[i] = stl ? (double)in.QN[i * NX + jx] : 0.0;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dot12(acc, eN, qn);
+      lam = sum4(acc);
+    }
+    ring2<SA>(N, true,
+        [&](int k, SA& s) {
+          const T* rows = cbase + (int64_t)k * cstride;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) s.cr[i] = rows[i * ABT2_W];
+          s.rf = refp[(int64_t)k * refs];
+        },
+        [&](int k, const SA& s) {
+          const double w = (stl ? (double)xs[k * NX + jx] : (double)us[k * NU + ju]) - (double)s.rf;
+          double col[NX], swc[NZ];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) col[i] = (double)s.cr[i];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) swc[i] = (double)SW[i * NZ + j];
+          double acc[4] = {0.0, 0.0, 0.0, 0.0};
+          dot12(acc, lam, col);
+          dot16(acc, w, swc);
+          const double g = sum4(acc);
+          if (stl) {
+            lam = g;
+          } else if (r < REF_STEPS) {
+            if (ver) dks[k * NU + ju] = (T)g;
+          } else {
+            double aa[4] = {0.0, 0.0, 0.0, 0.0};
+            dot12abs(aa, lam, col);
+            dot16abs(aa, w, swc);
+            const double tolp = REF_TOL * sum4(aa);
+            const bool lo = (lowm >> k) & 1u, hi = (upm >> k) & 1u;
+            const T uk = us[k * NU + ju];
+            rd |= (M)((lo && g < -tolp) || (hi && g > tolp)) << k;
+            alo |= (M)(!lo && !hi && uk < in.lbm - in.tol_u) << k;
+            ahi |= (M)(!lo && !hi && uk > in.ubm + in.tol_u) << k;
+          }
+        });
+    if (r == REF_STEPS) break;
+    // (2b) the correction's backward recursion (fp32): the masked Riccati recursion of the set for
+    // the linear term alone, d = -H_FF^{-1} g_F (P_{k+1}: QN, else the PS2 snapshot, which holds
+    // the current set's value function); dks: g_k in, the feedforward d_k out
+    struct SB { T cr[NX]; T ps[PS2_W]; };
+    T pc = T(0);   // state lanes: the correction's p_{k+1}
+    ring2<SB>(N, true,
+        [&](int k, SB& s) {
+          const T* rows = cbase + (int64_t)k * cstride;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) s.cr[i] = rows[i * ABT2_W];
+          ldv<T, PS2_W>(PS.at(k + 1 < N ? k + 1 : k) + jx * PS2_W, s.ps);
+        },
+        [&](int k, const SB& s) {
+          const bool lo = !stl && ((lowm >> k) & 1u), hi = !stl && ((upm >> k) & 1u);
+          T Pc[NX];
+          if (k == N - 1) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) Pc[i] = stl ? in.QN[i * NX + jx] : T(0);
+          } else {   // (unpacked through the group's LDS block, as at a restart)
+            if (stl) {
+#pragma unroll
+              for (int d = 0; d < PS2_W; ++d) PX[jx * PS2_W + d] = s.ps[d];
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+              const int dd = (jx - i + NX) % NX;
+              Pc[i] = stl ? PX[dd <= 6 ? i * PS2_W + dd : jx * PS2_W + (NX - dd)] : T(0);
+            }
+            wave_lds_sync();
+          }
+          // G = [A|B]^T P [A|B] + s blkdiag(Q, R) (lane j: column j), h = [A|B]^T p + (0, g)
+          float y[16], gg[16];
+          to_columns(outer12(Pc, s.cr), y);
+          to_columns(outer12(s.cr, y), gg);
+          T G[NZ];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) G[i] = gg[i] + SW[i * NZ + j];
+          T hj;
+          {
+            T ac[4] = {T(0), T(0), T(0), T(0)};
+            dot12(ac, pc, s.cr);
+            hj = sum4(ac) + (stl ? T(0) : dks[k * NU + ju]);
+          }
+          T Ht[NU * NU], ht[NU], Hux_t[NU];
+          static_for<NU>([&](auto mm) {
+            constexpr int m = decltype(mm)::value;
+            Ht[m * NU + 0] = bc<NX + 0>(G[NX + m]);
+            Ht[m * NU + 1] = bc<NX + 1>(G[NX + m]);
+            Ht[m * NU + 2] = bc<NX + 2>(G[NX + m]);
+            Ht[m * NU + 3] = bc<NX + 3>(G[NX + m]);
+            ht[m] = bc<NX + m>(hj);
+            Hux_t[m] = G[NX + m];
+          });
+          {   // fixed components: d = 0 (identity rows and columns, no gradient)
+            const int fx_own = (lo || hi) ? 1 : 0;
+            int fixed[NU];
+            fixed[0] = bc<NX + 0>(fx_own); fixed[1] = bc<NX + 1>(fx_own);
+            fixed[2] = bc<NX + 2>(fx_own); fixed[3] = bc<NX + 3>(fx_own);
+#pragma unroll
+            for (int m = 0; m < NU; ++m) {
+              ht[m] = fixed[m] ? T(0) : ht[m];
+              Hux_t[m] = fixed[m] ? T(0) : Hux_t[m];
+#pragma unroll
+              for (int n = 0; n < NU; ++n)
+                Ht[m * NU + n] = (fixed[m] || fixed[n]) ? ((m == n) ? T(1) : T(0)) : Ht[m * NU + n];
+            }
+          }
+          T Lc[10], kff[NU], nh[NU];
+          chol4(Ht, Lc);
+#pragma unroll
+          for (int m = 0; m < NU; ++m) nh[m] = -ht[m];
+          chol4_solve(Lc, nh, kff);
+          T pn = hj;
+#pragma unroll
+          for (int m = 0; m < NU; ++m) pn += Hux_t[m] * kff[m];
+          pc = stl ? pn : T(0);
+          if (!stl && ver) dks[k * NU + ju] = sel<NU>(kff, ju);
+        });
+    // (3) the correction's forward pass with the stored gains (KR2), fused with the next
+    // re-simulation: u_k += K_k (x_k - x_k^old) + d_k (input lanes), then x_{k+1} in fp64 from the
+    // refined u (state lanes; x_k^old: the previous re-simulation in xs)
+    struct SC { T pv[KR2_W]; T yb, gp; };
+    double zd = 0.0;
+    if (iterate && stl) zd = (double)in.x0[jx] - (double)XU.at(0)[jx * SS];
+    ring2<SC>(N, false,
+        [&](int k, SC& s) {
+          ldv<T, KR2_W, 8>(stl ? ABT.at(k) + jx * ABT2_W : KR.at(k) + ju * KR2_W, s.pv);
+          s.yb = XU.at(k)[j * SS];
+          s.gp = iterate ? GP.at(k)[jx * SS] : T(0);
+        },
+        [&](int k, const SC& s) {
+          // state lanes: the refined x_k minus the previous one (fp32 is enough for the gain product)
+          T dxs = T(0);
+          if (stl) {
+            const double xn = (double)s.yb + zd;
+            dxs = (T)(xn - (double)xs[k * NX + jx]);
+            if (ver) xs[k * NX + jx] = (T)xn;
+          }
+          T ac[4] = {stl ? T(0) : dks[k * NU + ju], T(0), T(0), T(0)};
+          T krow[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) krow[i] = s.pv[i];
+          dot12(ac, dxs, krow);
+          double zk = zd;
+          if (!stl) {
+            const T un = us[k * NU + ju] + sum4(ac);
+            if (ver) us[k * NU + ju] = un;
+            zk = (double)un - (double)s.yb;
+          }
+          double row[NZ];
+          arow(s.pv, row);
+          double acc[4] = {(double)s.gp, 0.0, 0.0, 0.0};
+          dot16(acc, zk, row);
+          if (stl) zd = sum4(acc);
+        });
+    if (stl && ver) xs[N * NX + jx] = (T)((double)XU.at(N)[jx * SS] + zd);
+  }
+  return RefOut<W32>{rd, alo, ahi};
+}
+
+// The refinement list (SplitArgs::as_ref): [0] count, [1] the refinement kernel's work counter,
+// then AS_REF_W words per entry -- chunk instance, passes, forward passes, backward stages, and
+// per input component m the stage masks of its lower (4 + 2m, + 1 for stages 32..63) and upper
+// (12 + 2m, ...) active sets.  Written by the 16 lanes of the instance's group.
+template <bool W32, class M>
+__device__ __forceinline__ void as_ref_put(int* e, int j, int c, int git, int n_fwd, int n_bst, M lowm, M upm) {
+  if (j == 0) {
+    e[0] = c;
+    e[1] = git;
+    e[2] = n_fwd;
+    e[3] = n_bst;
+  }
+  if (j >= NX) {
+    const int w = 4 + 2 * (j - NX);
+    e[w] = (int)(uint32_t)lowm;
+    e[w + 8] = (int)(uint32_t)upm;
+    if constexpr (!W32) {
+      e[w + 1] = (int)(uint32_t)((uint64_t)lowm >> 32);
+      e[w + 9] = (int)(uint32_t)((uint64_t)upm >> 32);
+    }
+  }
+}
+
+// REF: the refinement kernel (as_ref_kernel_f32, mpcb_as.hip): its groups take the instances the
+// active-set kernel listed in SplitArgs::as_ref (converged sets with an undecided multiplier),
+// restore their active sets and pass counts, redo the final forward pass (the same arithmetic:
+// the same U and multipliers) and run the refinement + verification below, iterating on where it
+// changes the set.  The active-set kernel itself only lists them: inlined there, the refinement's
+// registers spilled its pass loop (c4 kernel 3.44 vs 3.24 ms).
+template <class T, bool BOX, bool W32 = false, bool ITER = false, bool REF = false>
 __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   if constexpr (!BOX) AS_WT(0);
   // box kernel: the workspace and I/O pointers as opaque loop-invariant VGPRs (as P2's model
@@ -200,10 +520,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     a.KR = vglobal(a.KR); a.PS = vglobal(a.PS); a.xref = vglobal(a.xref); a.uref = vglobal(a.uref);
     a.u0 = vglobal(a.u0); a.X = vglobal(a.X); a.U = vglobal(a.U); a.status = vglobal(a.status);
     a.qp_stats = vglobal(a.qp_stats); a.x0 = vglobal(a.x0); a.as_fb = vglobal(a.as_fb);
+    a.as_ref = vglobal(a.as_ref);
   }
   using Mk = Masks<W32>;
   using M = typename Mk::M;
   constexpr int WB = Mk::WB;
+  constexpr bool UNC = BOX && sizeof(T) == 4;   // fp32 box: undecided multipliers are flagged
+  constexpr bool VER = UNC && REF;               // ... and refined + verified (REF kernel)
   __shared__ T lds_px[GROUPS][NX * NX];   // P_k by columns, for the symmetric transpose
   extern __shared__ __attribute__((aligned(16))) unsigned char as_dyn[];
   const int lane = threadIdx.x;
@@ -243,12 +566,19 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   const int tv = var_index(j);                      // variable column of [A|B] owned by lane j
   // constant directions read their column from W.ctab with the same strided loads (slot 0..5)
   const int cslot = j < 3 ? j : j - 3;
+  const int* ent = nullptr;   // REF: the group's list entry (AS_REF_W words, as_ref_put)
   auto bind = [&](int64_t c_raw) {
 #ifdef MPCB_AS_ORDER_DBG   // (tools/ab_as_order.py)
     if (a.as_order && c_raw < nb) c_raw = a.as_order[c_raw];
 #endif
-    valid = c_raw < nb;
-    c = valid ? c_raw : nb - 1;       // an empty group shadows the last instance
+    if constexpr (REF) {
+      valid = c_raw < a.as_ref[0];
+      ent = a.as_ref + AS_REF_HDR + (valid ? c_raw : 0) * AS_REF_W;
+      c = valid ? ent[0] : nb - 1;
+    } else {
+      valid = c_raw < nb;
+      c = valid ? c_raw : nb - 1;     // an empty group shadows the last instance
+    }
     b = a.b0 + c;
     xr = a.xref + b * a.xref_sb;
     ur = a.uref + b * a.uref_sb;
@@ -298,7 +628,29 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   int n_fwd = 0, n_bst = 0;
   int kc = -1;                  // highest stage whose active set changed (group-uniform)
   int git = 0;                  // passes of the group's current instance
-  bool u0fin = true;            // u0 of the flushed (final) pass is finite (staged outputs)
+  int rpass = 0;                // REF: refined passes of the group's current instance
+  // REF: the listed instance's active set and counts (as_ref_put)
+  auto restore = [&]() {
+    rpass = 0;
+    if constexpr (REF) {
+      if (valid) {
+        git = ent[1];
+        n_fwd = ent[2];
+        n_bst = ent[3];
+        const int w = 4 + 2 * ju;
+        if (!stl) {
+          lowm = (M)(uint32_t)ent[w];
+          upm = (M)(uint32_t)ent[w + 8];
+          if constexpr (!W32) {
+            lowm |= (M)(uint32_t)ent[w + 1] << 32;
+            upm |= (M)(uint32_t)ent[w + 9] << 32;
+          }
+        }
+      }
+    }
+  };
+  restore();
+  bool u0fin = true;           // u0 of the flushed (final) pass is finite (staged outputs)
   // (the box kernel: always -- mpcb_create refuses box_u beyond N = 64 and mpcb_solve X / U that
   // are not 16-B aligned -- so its stage loop carries no direct-store path)
   const bool stage_out = BOX || (N <= OUT_NMAX && ((((uintptr_t)a.X) | ((uintptr_t)a.U)) & 15) == 0);
@@ -587,9 +939,12 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
 
     // ------------------------------------------------ forward pass, multipliers, violations
     M vlo = 0, vhi = 0, vfl = 0, vfu = 0;   // input lanes: violation sets of component ju
+    // (fp32 box) input lanes: a fixed component's multiplier lies within its rounding bound
+    // tol_mu, so the pass's KKT test cannot decide its sign (verified below)
+    bool unc = false;
     const bool write = valid && !done;
     // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
-    T* const xs = reinterpret_cast<T*>(as_dyn) + q * out_elems<T>(N);   // X rows, then U rows
+    T* const xs = reinterpret_cast<T*>(as_dyn) + q * (BOX ? box_elems<T>(N) : out_elems<T>(N));   // X rows, then U rows
     T* const us = xs + (N + 1) * NX;
     T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
     if (iterate && stl) zj = a.x0[b * a.x0_sb + jx] - XU.at(0)[jx * SS];
@@ -686,8 +1041,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       T tol_mu = T(0);
       // the rounding bound of mu matters only where its sign is wrong for its side (elsewhere
       // the test below fails whatever the tolerance): computed only when some lane of the wave
-      // has such a multiplier (wave-uniform: the DPP block needs whole rows)
-      if (BOX && __builtin_amdgcn_ballot_w64((lo && v < T(0)) || (hi && v > T(0)))) {
+      // has such a multiplier (wave-uniform: the DPP block needs whole rows).  fp32: wherever a
+      // component is fixed, since a right-sign multiplier within the bound is undecided too (the
+      // fp32 Riccati form carries errors of 0.35 tol_mu by stage 2 of 30)
+      if (BOX && __builtin_amdgcn_ballot_w64(UNC ? (lo || hi) : ((lo && v < T(0)) || (hi && v > T(0))))) {
         T aa[4] = {T(fabs(r0)), T(0), T(0), T(0)};
         dot16abs(aa, zj, row);
         tol_mu = T(64) * eps * sum4(aa);
@@ -700,6 +1057,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         vhi |= (M)(fr && yo > ubm + tol_u) << k;
         vfl |= (M)(lo && mu < -tol_mu) << k;
         vfu |= (M)(hi && mu > tol_mu) << k;
+        if constexpr (UNC) unc = unc || ((lo || hi) && fabs(mu) <= tol_mu);
       } else {
         zj = v;
       }
@@ -744,6 +1102,89 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     if (!BOX && stage_out && write) flush_out();
     if constexpr (!BOX) break;
 
+    // ------------------------------------------------ fp64-residual refinement + KKT verification (fp32 box)
+    // (REF kernel: every pass.)  A converged fp32 pass with a fixed component whose multiplier lies
+    // within its rounding bound tol_mu = 64 eps sum|terms| has not decided that component: the Riccati-form multiplier
+    // h_u + G_ux dx + G_uu du sums terms ~10 that cancel to ~1e-4, while the component's curvature
+    // can be as small as s R (1.7e-3 at the last stage), so an undecided multiplier of -8e-5 leaves
+    // u 0.03 N off the minimiser.  c4 (tools/c4_full_parity.py): 24 of 65,536 instances beyond 5e-5
+    // in U, each with one component fixed at a bound that the exact solution leaves free.  Neither
+    // the fp32 data nor the rollout is the cause (the exact QP on the device's fp32 [A|B] is 1.8e-7
+    // off; an fp64 rollout changes nothing: tools/box_verify_debug.py): the fp32 solve's own error
+    // in the free components (~1e-3 N) moves the gradient at the fixed ones by ~8e-5.  So:
+    //   r = 0  refinement: the objective's exact gradient g at the pass's U in fp64 over the same
+    //          fp32 stage data (states re-simulated from U, then the adjoint sweep
+    //          lambda_N = QN e_N, g_k = [A|B]_k^T lambda_{k+1} + s blkdiag(Q, R)(e_k, u_k - uref_k)),
+    //          then the correction d = -H_FF^{-1} g_F on the free components by the fp32 Riccati
+    //          recursion of the same set (P_{k+1} from the PS2 snapshots, which hold the current
+    //          set's value function: the linear-term recursion only, no gap, d x_0 = 0) and a
+    //          forward pass with the stored gains (KR2): U += d;
+    //   r = 1  verification: g again at the refined U.  Fixed components whose multiplier has the
+    //          wrong sign beyond 2^-20 of its terms' sum (~0.3) and free components beyond their
+    //          bound by more than tol_u are this pass's violation sets, in place of the fp32
+    //          forward pass's (which is what cannot decide them: after a release the fp32 pass
+    //          put the released component back below its bound, and 27 of 157 c4 instances
+    //          cycled), and the Kim-Park update below proceeds on them.
+    // The active-set kernel lists the instances whose converged set has an undecided multiplier
+    // (as_ref_put); the refinement kernel restores each set, redoes its final forward pass and runs
+    // every further pass this way.  Each refinement is counted as six forward passes in qp_stats.
+    // The output X of a refined instance is the fp64 re-simulation of its U.
+    // Oracle: oracle.ocp.pdas_solve (the exact-arithmetic active set).
+    if constexpr (VER) {
+      const bool ver = write;
+      if (__builtin_amdgcn_ballot_w64(ver)) {   // (wave-uniform: the DPP blocks need whole rows)
+        // the refinement's stage loops read their records one stage at a time (no prefetch ring):
+        // bring the group's records into L2 first, all loads in flight at once (lane j touches
+        // stages j, j + 16, ...: one dword per 128-B line), so those loops wait on L2, not HBM
+        if (ver) {
+          T acc = T(0);
+          for (int k = j; k <= N; k += 16) {
+            T v[16];
+            const int kk = k < N ? k : N - 1;
+            const T* ab = ABT.at(kk);
+            const T* kr = KR.at(kk);
+            const T* ps = PS.at(kk);
+            const T* xu = XU.at(k);
+            v[0] = ab[0]; v[1] = ab[32]; v[2] = ab[64]; v[3] = ab[96]; v[4] = ab[ABT2_REC - 1];
+            v[5] = kr[0]; v[6] = kr[32]; v[7] = kr[KR2_REC - 1];
+            v[8] = ps[0]; v[9] = ps[32]; v[10] = ps[64]; v[11] = ps[PS2_REC - 1];
+            v[12] = xu[0]; v[13] = xu[32];
+            v[14] = iterate ? GP.at(kk)[0] : T(0);
+            v[15] = xr[(int64_t)k * NX];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc += v[i];
+          }
+          asm volatile("" ::"v"(acc));
+        }
+        RefIn<W32> in{a.x0 + b * a.x0_sb, XU, GP, ABT, KR, PS, cbase, cstride, refp, refs, xrN, W.QN,
+                      SW, PX, xs, us, us + N * NU,
+                      {crow[0], crow[1], crow[2], crow[3], crow[4], crow[5]},
+                      lowm, upm, lbm, ubm, tol_u, N, iterate, ver};
+        const RefOut<W32> ro = refine_verify<W32>(in);
+        // after REF_PASSES refined passes the multiplier verdicts are dropped: a component whose
+        // release and re-fix alternate (a 2-cycle on 20 of 157 c4 instances: the exact multiplier
+        // +1.7e-6, within the refinement's accuracy on fp32 data) stays at its bound, which moves
+        // the solution by |mu| / s R ~ 1e-3 N at most
+        const M rd = rpass < REF_PASSES ? ro.rd : M(0), alo = ro.alo, ahi = ro.ahi;
+        ++rpass;
+#if defined(MPCB_REF_TRACE) && defined(MPCB_AS_OWNER)   // (diagnostic builds: the passes of chunk instance MPCB_REF_TRACE)
+        if (ver && c == MPCB_REF_TRACE && git < 128) {
+          if (!stl) {
+            int* t = g_ref_trace[git] + 5 * ju;
+            t[0] = (int)(uint32_t)lowm; t[1] = (int)(uint32_t)upm;
+            t[2] = (int)(uint32_t)rd; t[3] = (int)(uint32_t)alo; t[4] = (int)(uint32_t)ahi;
+          }
+        }
+#endif
+        if (ver) {
+          n_fwd += 6;
+          vlo = alo;
+          vhi = ahi;
+          vfl = rd & lowm;
+          vfu = rd & upm;
+        }
+      }
+    }
     // ------------------------------------------------ active-set update (Kim-Park)
     const M V = vlo | vhi | vfl | vfu;
     const int cnt = stl ? 0 : Mk::popc(V);
@@ -775,11 +1216,12 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     // restart at kc + 1 from the snapshot there: the last pass that recomputed that stage, or
     // (never recomputed: its active set is still empty) P2's unconstrained pass
     kc = changed ? WB - 1 - Mk::clz(changed) : -1;
+    const bool cvd = gconv;   // converged (the refinement kernel: on the refined violation sets)
     // the instance is finished: converged, or the pass cap
     // (or, with the fallback, the first pass violates more than 7/20 of the horizon's input
     // components: oracle.ocp.AS_IPM_NV_NUM / _DEN, a strongly constrained QP)
     const bool crowded = BOX && a.as_fb && git == 0 && nV * AS_IPM_NV_DEN > AS_IPM_NV_NUM * N * NU;
-    const bool fin_now = write && (gconv || git + 1 >= a.max_as_iter || crowded);
+    const bool fin_now = write && (cvd || git + 1 >= a.max_as_iter || crowded);
     if (stage_out && fin_now) flush_out();
     wave_lds_sync();   // the next pass's staging writes follow the flush's LDS reads
     ++git;
@@ -787,16 +1229,37 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       // not converged within the pass budget (min(max_as_iter, AS_IPM_AFTER), mpcb_capi.hip): the
       // interior point takes the instance over (mpcb_asipm.h, oracle.ocp.pdas_solve) unless a
       // factorisation failed; the status is then the fallback's to write
-      const bool to_ipm = BOX && !gconv && st == MPCB_STATUS_OK && a.as_fb;
+      const bool to_ipm = BOX && !cvd && st == MPCB_STATUS_OK && a.as_fb;
       if (to_ipm) {
         if (j == 0) a.as_fb[2 + atomicAdd(a.as_fb, 1)] = (int)c;
-      } else if (!gconv) {
+      } else if (!cvd) {
         st = (st == MPCB_STATUS_OK) ? MPCB_STATUS_MAXITER : st;
+      }
+      if constexpr (UNC && !REF) {
+        // a converged set with an undecided multiplier: listed for the refinement kernel (its
+        // outputs are written here as well, and overwritten there)
+        // ... or whose first-stage controls are all below AS_REF_U0 (the test's normwise error of
+        // u0 divides by max(|u0|, 1): there fp32's ~1e-4 N absolute error counts in full -- 6 of
+        // c4's 65,536 instances beyond 5e-5, all with |u0| < 1.5 N; 95 have |u0| < 2 N)
+        const int so = (!stl && fabs(us[ju]) < T(AS_REF_U0)) ? 1 : 0;
+        const bool small = (bc<NX + 0>(so) & bc<NX + 1>(so)) & (bc<NX + 2>(so) & bc<NX + 3>(so));
+        const int un = unc ? 1 : 0;
+        const bool lst = cvd && a.as_ref &&
+                         (small || ((bc<NX + 0>(un) | bc<NX + 1>(un)) | (bc<NX + 2>(un) | bc<NX + 3>(un))));
+        if (lst) {   // (group-uniform: the row broadcast below has its 16 lanes)
+          int t = 0;
+          if (j == 0) t = atomicAdd(a.as_ref, 1);
+          t = bc<0>(t);
+          as_ref_put<W32>(a.as_ref + AS_REF_HDR + (int64_t)t * AS_REF_W, j, (int)c, git, n_fwd, n_bst, lowm, upm);
+        }
       }
       finish(!to_ipm);
       // the next instance of the chunk (lane 0 of the group draws it), else the group stays empty
       int nxt = (int)nb;
-      if (a.as_queue) {
+      if constexpr (REF) {
+        if (j == 0) nxt = (int)gridDim.x * GROUPS + atomicAdd(a.as_ref + 1, 1);
+        nxt = bc<0>(nxt);
+      } else if (a.as_queue) {
         if (j == 0) nxt = (int)gridDim.x * GROUPS + atomicAdd(a.as_queue, 1);
         nxt = bc<0>(nxt);
       }
@@ -808,6 +1271,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       n_fwd = n_bst = 0;
       kc = -1;
       git = 0;
+      restore();
       u0fin = true;
       done = !valid;
     } else if (!valid) {

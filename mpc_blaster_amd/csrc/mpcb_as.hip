@@ -34,6 +34,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS
 as_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true, W32, ITER>(a); }
 template <bool W32, bool ITER = false>
 __global__ void __launch_bounds__(64) as_kernel_f64(SplitArgs<double> a) { asq::as_body<double, true, W32, ITER>(a); }
+// the fp32 refinement of the listed instances (mpcb_as.h as_body REF)
+template <bool W32, bool ITER = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MPCB_AS_WAVES, 8)))
+as_ref_kernel_f32(SplitArgs<float> a) { asq::as_body<float, true, W32, ITER, true>(a); }
 template <class T, bool ITER = false>
 __global__ void __launch_bounds__(64) fwd_rm_kernel(SplitArgs<T> a) { asq::as_body<T, false, false, ITER>(a); }
 template <class T, bool ITER = false>
@@ -44,7 +48,7 @@ as_ipm_kernel(SplitArgs<T> a) {
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
+  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::box_elems<T>(a.N) * sizeof(T) : 0;
   if (a.as_queue && !dry_run()) {   // as many waves as stay resident; the rest of the chunk comes off the counter
     static const unsigned resident = [] {
       int dev = 0, cus = 0;
@@ -59,6 +63,10 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   }
   if (a.as_fb && !dry_run()) {   // the interior-point fallback's list starts empty
     const hipError_t e = hipMemsetAsync(a.as_fb, 0, 2 * sizeof(int), st);
+    if (e != hipSuccess) return e;
+  }
+  if (a.as_ref && !dry_run()) {   // the refinement list starts empty
+    const hipError_t e = hipMemsetAsync(a.as_ref, 0, AS_REF_HDR * sizeof(int), st);
     if (e != hipSuccess) return e;
   }
   const bool w32 = a.N <= 32;   // (the stage masks fit 32 bits)
@@ -78,6 +86,28 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
     } else {
       if (w32) MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<true>), dim3(g), dim3(64), lds, st, a);
       else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<false>), dim3(g), dim3(64), lds, st, a);
+    }
+  }
+  // the listed fp32 instances' refinement (a few hundred of c4's 65,536; before the fallback, to
+  // which it can hand an instance over).  Not in the launch log either (below).
+  if constexpr (sizeof(T) == 4) {
+    if (a.as_ref && !dry_run()) {
+      static const unsigned resident_ref = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+          cus = 256;
+        return (unsigned)cus * 4u * (unsigned)MPCB_AS_WAVES;
+      }();
+      unsigned gr = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+      if (gr > resident_ref) gr = resident_ref;
+      if (it) {
+        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true, true>), dim3(gr), dim3(64), lds, st, a);
+        else hipLaunchKernelGGL((as_ref_kernel_f32<false, true>), dim3(gr), dim3(64), lds, st, a);
+      } else {
+        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true>), dim3(gr), dim3(64), lds, st, a);
+        else hipLaunchKernelGGL((as_ref_kernel_f32<false>), dim3(gr), dim3(64), lds, st, a);
+      }
     }
   }
   // the instances the active set handed over (usually none: the waves read an empty list and
@@ -114,6 +144,11 @@ template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb
 
+#ifdef MPCB_REF_TRACE
+extern "C" int mpcb_debug_ref_trace(int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_ref_trace), sizeof(int) * 128 * 20) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef MPCB_STAMPS
 extern "C" int mpcb_debug_wt_p3(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_wt_p3), sizeof(unsigned long long) * MPCB_WT_MAX * 7) == hipSuccess ? 0 : -2;

@@ -346,8 +346,10 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   }
   if (cfg->box_u && (full || h->split)) {
     // (+ 16: the 12/4 active-set kernel's work counter after the statistics; then its
-    // interior-point fallback's list, 2 + max_batch: SplitArgs::as_fb)
-    e = hipMalloc((void**)&h->qp_stats, ((size_t)max_batch * 3 + 18) * sizeof(int32_t));
+    // interior-point fallback's list, 2 + max_batch: SplitArgs::as_fb; then the fp32 refinement
+    // list, AS_REF_HDR + AS_REF_W max_batch: SplitArgs::as_ref)
+    e = hipMalloc((void**)&h->qp_stats,
+                  ((size_t)max_batch * (3 + AS_REF_W) + 18 + AS_REF_HDR) * sizeof(int32_t));
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
       (void)hipFree(h->weights);
@@ -381,6 +383,15 @@ extern "C" int mpcb_debug_set_as_order(mpcb_handle* h, const int32_t* dev_order)
   return MPCB_OK;
 }
 #endif
+// Diagnostic (not part of the ABI header): the last fp32 input-box chunk's refinement list header
+// (mpcb_kernels.h AS_REF_*: [0] instances listed, [1] the refinement kernel's counter), read
+// synchronously into out[0..1] (tools/c4_full_parity.py).
+extern "C" int mpcb_debug_ref_list(mpcb_handle* h, int32_t* out) {
+  if (!h || !h->qp_stats || !out) return fail(MPCB_E_INVALID, "no input-box handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpy(out, h->qp_stats + 3 * h->max_batch + 18, 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return MPCB_OK;
+}
 extern "C" int mpcb_qp_stats(mpcb_handle* h, int64_t B, int32_t* out, void* stream) {
   if (!h) return fail(MPCB_E_INVALID, "null handle");
   if (!h->qp_stats) return fail(MPCB_E_UNSUPPORTED, "QP statistics are kept by input-box handles");
@@ -483,6 +494,8 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.as_queue = h->qp_stats ? h->qp_stats + 2 * h->max_batch : nullptr;
       if (const char* e = getenv("MPCB_AS_PERSIST")) if (atoi(e) == 0) a.as_queue = nullptr;
       a.as_fb = (h->cfg.box_u && h->qp_stats) ? h->qp_stats + 2 * h->max_batch + 16 : nullptr;
+      a.as_ref = (sizeof(T) == 4 && h->cfg.box_u && h->qp_stats) ? h->qp_stats + 3 * h->max_batch + 18 : nullptr;
+      if (const char* e = getenv("MPCB_AS_REFINE")) if (atoi(e) == 0) a.as_ref = nullptr;   // (A/B: no refinement)
       a.as_order = (h->cfg.box_u && b0 == 0) ? h->as_order_dbg : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);

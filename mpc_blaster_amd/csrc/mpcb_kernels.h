@@ -130,6 +130,11 @@ constexpr int AS_IPM_AFTER = 48;
 // ... or after the first pass when it violates more than 7/20 of the horizon's input components
 // (oracle.ocp.AS_IPM_NV_NUM / _DEN)
 constexpr int AS_IPM_NV_NUM = 7, AS_IPM_NV_DEN = 20;
+// the fp32 input box's refinement list (SplitArgs::as_ref, mpcb_as.h as_ref_put): a header of
+// AS_REF_HDR words, then AS_REF_W per listed instance
+constexpr int AS_REF_HDR = 4, AS_REF_W = 20;
+// ... which also lists converged instances whose first-stage controls are all below this (N)
+constexpr double AS_REF_U0 = 2.0;
 
 template <class T>
 struct SplitArgs {
@@ -155,6 +160,8 @@ struct SplitArgs {
   const int32_t* as_order;   // (MPCB_AS_ORDER_DBG builds, nullable) ticket -> chunk instance
   int* as_fb;        // box path (nullable): the interior-point fallback's list ([0] count, [2 + t]
                      // chunk instance), filled by the active-set kernel (mpcb_asipm.h)
+  int* as_ref;       // fp32 box path (nullable): the refinement list (mpcb_as.h AS_REF_*), filled by
+                     // the active-set kernel, walked by the refinement kernel
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout

@@ -81,6 +81,27 @@ def test_bench_gpus_4_adds_the_c4_secondary(tmp_path):
     assert np.array_equal(got, ref)
 
 
+def test_bench_gpus_8_adds_the_c5_histogram_secondary(tmp_path):
+    """At 8 ranks the line also times BASELINE configs[4] (c5: N = 40, fp32, wind, instance-sharded
+    over 8 GPUs with only the u0* histogram reduced, bench.py sec_name): the all-reduced per-motor
+    histogram equals the global oracle histogram of all 8 shards' instances, bit for bit."""
+    from oracle.inputs import make_inputs
+    from oracle.ocp import OcpSpec, mpc_solve
+    sb = 3
+    line, _ = _run_bench(tmp_path, 'c2', 8, 2, steps=1, extra=['--secondary-batch', str(sb)])
+    assert line['n_gpus'] == 8 and line['config']['global_batch'] == 16
+    sec = line['secondary']
+    assert sec['workload'].startswith('c5') and sec['global_batch'] == 8 * sb and sec['n_gpus'] == 8
+    assert sec['value'] > 0 and sec['bad_status'] == 0
+    got = np.load(str(tmp_path / 'gather_c2.npy') + '.secondary.npy')
+    inp = make_inputs('c5', ids=np.arange(8 * sb, dtype=np.uint64), N=40)
+    ref = mpc_solve(inp['x0'], inp['xref'], inp['uref'], OcpSpec(N=40), wind=inp['wind'])['u0']
+    b = np.clip(np.floor(ref * (64 / 65.0)), 0, 63).astype(np.int64)
+    want = np.stack([np.bincount(b[:, m], minlength=64) for m in range(4)])
+    assert got.shape == (4, 64) and got.sum() == 4 * 8 * sb
+    assert np.array_equal(got, want)
+
+
 def test_bench_stalled_rank_fails_fast():
     """A rank that never joins the rendezvous: the others give up after --init-timeout and the
     parent exits non-zero well before the driver's limit (no hang, no JSON line)."""
