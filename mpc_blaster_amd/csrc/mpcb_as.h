@@ -156,10 +156,10 @@ template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int6
 // waited for the write acknowledgements of the previous stages' scattered 4/8-B output stores.
 constexpr int OUT_NMAX = 64;   // longer horizons store directly
 template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
-// the box kernel's block per instance: the staged rows, then (fp32) the refinement's N x NU
-// feedforward terms
-template <class T> __host__ __device__ constexpr int box_elems(int N) {
-  return out_elems<T>(N) + (sizeof(T) == 4 ? N * NU : 0);
+// the refinement kernel's block per instance: the staged rows, then the refinement's N x NU
+// feedforward terms and (N + 1) x NX state errors x - xref
+template <class T> __host__ __device__ constexpr int ref_elems(int N) {
+  return out_elems<T>(N) + N * NU + (N + 1) * NX;
 }
 
 // Stage masks (active sets, violations: bit k = stage k) of a horizon N <= 32 in 32-bit registers
@@ -205,9 +205,11 @@ template <class P> __device__ __forceinline__ P* vglobal(P* p) {
 // with ver = false compute along and write nothing.  Its stage loops are latency chains over a
 // few hundred instances, so each keeps its next stage's loads in flight (two register slots, the
 // loop unrolled by two, as the active-set kernel's backward pass).
-// refinement steps per pass before the verification, the refined passes whose multiplier verdicts
-// count, and the verification's tolerance on a multiplier relative to its terms' sum
-constexpr int REF_STEPS = 1, REF_PASSES = 3;
+// refinement steps per pass before the verification (up to REF_STEPS_MAX when the verification
+// would release a component: one more step before acting on it), the refined passes whose
+// multiplier verdicts count, and the verification's tolerance on a multiplier relative to its
+// terms' sum
+constexpr int REF_STEPS = 1, REF_STEPS_MAX = 1, REF_PASSES = 3;
 constexpr double REF_TOL = 0x1p-18;
 template <bool W32> struct RefIn {
   using M = typename Masks<W32>::M;
@@ -221,13 +223,14 @@ template <bool W32> struct RefIn {
   const T* SW;                       // s blkdiag(Q, R) (LDS)
   T* PX;                             // the group's P block (LDS)
   T* xs; T* us; T* dks;              // the group's staged X rows, U rows, refinement feedforward (LDS)
+  T* es;                             // ... and state errors x - xref (LDS)
   T crow[6];
   M lowm, upm;
   T lbm, ubm, tol_u;
   int N;
   bool iterate, ver;
 };
-template <bool W32> struct RefOut { typename Masks<W32>::M rd, alo, ahi; };
+template <bool W32> struct RefOut { typename Masks<W32>::M rd, alo, ahi; int sweeps; };
 
 // run body(k, slot) for k = k0, k0 + dir, ... (N stages) with load(k, slot) one stage ahead in two
 // register slots (every slot a fixed register set; loads for stages outside [0, N) are clamped)
@@ -270,6 +273,9 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
   T* const xs = in.xs;
   T* const us = in.us;
   T* const dks = in.dks;
+  // the adjoint reads the state errors e = x - xref rounded to fp32, not x: rounding x itself
+  // (|x| ~ 1, e ~ 1e-2) put ~1e-6 of noise into the multipliers through Q e
+  T* const es = in.es;
   const M lowm = in.lowm, upm = in.upm;
   T crow[6];
 #pragma unroll
@@ -287,7 +293,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
   M rd = 0, alo = 0, ahi = 0;   // input lanes: released stages, free components beyond a bound
 
   // (1) the states re-simulated in fp64 from the staged U, x_k into xs
-  struct SF { T rv[NVAR]; T yb, gp; };
+  struct SF { T rv[NVAR]; T yb, gp, rf; };
   {
     double zd = 0.0;   // state lanes dx_i, input lanes du_m
     if (iterate && stl) zd = (double)in.x0[jx] - (double)XU.at(0)[jx * SS];
@@ -296,26 +302,38 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           ldv<T, NVAR, 8>(ABT.at(k) + jx * ABT2_W, s.rv);
           s.yb = XU.at(k)[j * SS];
           s.gp = iterate ? GP.at(k)[jx * SS] : T(0);
+          s.rf = refp[(int64_t)k * refs];
         },
         [&](int k, const SF& s) {
           double row[NZ];
           arow(s.rv, row);
-          if (!stl) zd = (double)us[k * NU + ju] - (double)s.yb;
-          else if (ver) xs[k * NX + jx] = (T)((double)s.yb + zd);
+          if (!stl) {
+            zd = (double)us[k * NU + ju] - (double)s.yb;
+          } else if (ver) {
+            const double xk = (double)s.yb + zd;
+            xs[k * NX + jx] = (T)xk;
+            es[k * NX + jx] = (T)(xk - (double)s.rf);
+          }
           double acc[4] = {(double)s.gp, 0.0, 0.0, 0.0};
           dot16(acc, zd, row);
           if (stl) zd = sum4(acc);
         });
-    if (stl && ver) xs[N * NX + jx] = (T)((double)XU.at(N)[jx * SS] + zd);
+    if (stl && ver) {
+      const double xN = (double)XU.at(N)[jx * SS] + zd;
+      xs[N * NX + jx] = (T)xN;
+      es[N * NX + jx] = (T)(xN - (double)in.xrN[jx]);
+    }
   }
   struct SA { T cr[NX]; T rf; };
-  for (int r = 0; r <= REF_STEPS; ++r) {
+  int sweeps = 1;   // stage loops run (qp_stats counts each as a forward pass)
+  for (int r = 0;; ++r) {
+    ++sweeps;
     // (2) the adjoint sweep (fp64): lambda_N = QN e_N, g_k = [A|B]_k^T lambda_{k+1} + s blkdiag(Q,
     // R)(e_k, u_k - uref_k); r < REF_STEPS keeps the input lanes' g_k for the correction (dks),
     // r = REF_STEPS decides
     double lam;
     {
-      const double eN = stl ? (double)xs[N * NX + jx] - (double)in.xrN[jx] : 0.0;
+      const double eN = stl ? (double)es[N * NX + jx] : 0.0;
       double qn[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) qn[i] = stl ? (double)in.QN[i * NX + jx] : 0.0;
@@ -331,7 +349,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           s.rf = refp[(int64_t)k * refs];
         },
         [&](int k, const SA& s) {
-          const double w = (stl ? (double)xs[k * NX + jx] : (double)us[k * NU + ju]) - (double)s.rf;
+          const double w = stl ? (double)es[k * NX + jx] : (double)us[k * NU + ju] - (double)s.rf;
           double col[NX], swc[NZ];
 #pragma unroll
           for (int i = 0; i < NX; ++i) col[i] = (double)s.cr[i];
@@ -343,9 +361,10 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           const double g = sum4(acc);
           if (stl) {
             lam = g;
-          } else if (r < REF_STEPS) {
-            if (ver) dks[k * NU + ju] = (T)g;
           } else {
+            if (ver) dks[k * NU + ju] = (T)g;
+          }
+          if (!stl && r >= REF_STEPS) {
             double aa[4] = {0.0, 0.0, 0.0, 0.0};
             dot12abs(aa, lam, col);
             dot16abs(aa, w, swc);
@@ -357,7 +376,12 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
             ahi |= (M)(!lo && !hi && uk > in.ubm + in.tol_u) << k;
           }
         });
-    if (r == REF_STEPS) break;
+    // decided, unless a release is pending and another step is left (wave-uniform)
+    if (r >= REF_STEPS) {
+      if (r == REF_STEPS_MAX || !__builtin_amdgcn_ballot_w64(ver && rd != 0)) break;
+      rd = alo = ahi = 0;
+    }
+    sweeps += 2;
     // (2b) the correction's backward recursion (fp32): the masked Riccati recursion of the set for
     // the linear term alone, d = -H_FF^{-1} g_F (P_{k+1}: QN, else the PS2 snapshot, which holds
     // the current set's value function); dks: g_k in, the feedforward d_k out
@@ -440,7 +464,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
     // (3) the correction's forward pass with the stored gains (KR2), fused with the next
     // re-simulation: u_k += K_k (x_k - x_k^old) + d_k (input lanes), then x_{k+1} in fp64 from the
     // refined u (state lanes; x_k^old: the previous re-simulation in xs)
-    struct SC { T pv[KR2_W]; T yb, gp; };
+    struct SC { T pv[KR2_W]; T yb, gp, rf; };
     double zd = 0.0;
     if (iterate && stl) zd = (double)in.x0[jx] - (double)XU.at(0)[jx * SS];
     ring2<SC>(N, false,
@@ -448,6 +472,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           ldv<T, KR2_W, 8>(stl ? ABT.at(k) + jx * ABT2_W : KR.at(k) + ju * KR2_W, s.pv);
           s.yb = XU.at(k)[j * SS];
           s.gp = iterate ? GP.at(k)[jx * SS] : T(0);
+          s.rf = refp[(int64_t)k * refs];
         },
         [&](int k, const SC& s) {
           // state lanes: the refined x_k minus the previous one (fp32 is enough for the gain product)
@@ -455,7 +480,10 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           if (stl) {
             const double xn = (double)s.yb + zd;
             dxs = (T)(xn - (double)xs[k * NX + jx]);
-            if (ver) xs[k * NX + jx] = (T)xn;
+            if (ver) {
+              xs[k * NX + jx] = (T)xn;
+              es[k * NX + jx] = (T)(xn - (double)s.rf);
+            }
           }
           T ac[4] = {stl ? T(0) : dks[k * NU + ju], T(0), T(0), T(0)};
           T krow[NX];
@@ -474,9 +502,13 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           dot16(acc, zk, row);
           if (stl) zd = sum4(acc);
         });
-    if (stl && ver) xs[N * NX + jx] = (T)((double)XU.at(N)[jx * SS] + zd);
+    if (stl && ver) {
+      const double xN = (double)XU.at(N)[jx * SS] + zd;
+      xs[N * NX + jx] = (T)xN;
+      es[N * NX + jx] = (T)(xN - (double)in.xrN[jx]);
+    }
   }
-  return RefOut<W32>{rd, alo, ahi};
+  return RefOut<W32>{rd, alo, ahi, sweeps};
 }
 
 // The refinement list (SplitArgs::as_ref): [0] count, [1] the refinement kernel's work counter,
@@ -572,7 +604,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     if (a.as_order && c_raw < nb) c_raw = a.as_order[c_raw];
 #endif
     if constexpr (REF) {
-      valid = c_raw < a.as_ref[0];
+      valid = c_raw < a.as_ref[0] && c_raw < a.as_ref_cap;
       ent = a.as_ref + AS_REF_HDR + (valid ? c_raw : 0) * AS_REF_W;
       c = valid ? ent[0] : nb - 1;
     } else {
@@ -629,11 +661,18 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   int kc = -1;                  // highest stage whose active set changed (group-uniform)
   int git = 0;                  // passes of the group's current instance
   int rpass = 0;                // REF: refined passes of the group's current instance
-  // REF: the listed instance's active set and counts (as_ref_put)
+  M relm = 0, pin = 0;          // REF, input lanes: stages released by the refinement; fixed again after
+  // REF: the listed instance's active set and counts (as_ref_put), and its U (the output the
+  // active-set kernel wrote: mpcb_solve passes a U buffer of the handle's when the caller has none)
   auto restore = [&]() {
     rpass = 0;
+    relm = pin = 0;
     if constexpr (REF) {
       if (valid) {
+        T* const us0 = reinterpret_cast<T*>(as_dyn) + q * ref_elems<T>(N) + (N + 1) * NX;
+        const T* const ub = a.U + b * (int64_t)N * NU;
+        for (int e = j; e < N * NU; e += NZ) us0[e] = ub[e];
+        wave_lds_sync();
         git = ent[1];
         n_fwd = ent[2];
         n_bst = ent[3];
@@ -686,7 +725,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       kmax = o > kmax ? o : kmax;
     }
     if (git > 0 && !done && kc >= 0) n_bst += kc + 1;
-    if (!done) ++n_fwd;
+    if (!done && !REF) ++n_fwd;
     // ------------------------------------------------ masked Riccati over the cached [A|B]
     ASTAMP(7);
     if (BOX && kmax >= 0) {   // (a group in its first pass has kc = -1)
@@ -944,7 +983,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     bool unc = false;
     const bool write = valid && !done;
     // LDS staging of this pass's outputs (launch_*: dynamic LDS when N <= OUT_NMAX)
-    T* const xs = reinterpret_cast<T*>(as_dyn) + q * (BOX ? box_elems<T>(N) : out_elems<T>(N));   // X rows, then U rows
+    T* const xs = reinterpret_cast<T*>(as_dyn) + q * (REF ? ref_elems<T>(N) : out_elems<T>(N));   // X rows, then U rows
     T* const us = xs + (N + 1) * NX;
     T zj = T(0);   // state lanes: dx_j; input lanes: du_ju
     if (iterate && stl) zj = a.x0[b * a.x0_sb + jx] - XU.at(0)[jx * SS];
@@ -981,8 +1020,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     // a converged group rides along with its wave's other groups: its loads are skipped and its
     // results (garbage) neither written nor used
     const bool fetch = !BOX || !done;
-    if (fetch) gload(0);
-    static_for<FD>([&](auto s) { rload(decltype(s)::value < N ? decltype(s)::value : N - 1, s); });
+    if constexpr (!REF) {   // (the refinement kernel has no fp32 forward pass: the refinement's
+                            // correction from the previous point is this set's Newton step)
+      if (fetch) gload(0);
+      static_for<FD>([&](auto s) { rload(decltype(s)::value < N ? decltype(s)::value : N - 1, s); });
+    }
     auto stage = [&](int k, auto slot_tag) {
       constexpr int sl = decltype(slot_tag)::value;
       // the lane's row of the dot below: a state lane's row of [A|B] (variable columns loaded,
@@ -1021,6 +1063,10 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         zj = csel(mst, zj, sum4(acc));
       }
       const T yo = yb + zj;   // state lanes: x_k = xbar_k + dx_k; input lanes: u_k
+      // (Measured and dropped, round 6: a projected first pass -- a component beyond its bound
+      // clamped as the pass goes -- cut c4's forward passes 3.83 -> 3.48 per instance and its
+      // backward stages 1 %, the kernel time not at all (3.19 vs 3.20 ms), and its fuller first
+      // violation sets sent 120 instead of 26 of the 192 hard wind + sine draws to the fallback.)
       if (stage_out) {
         if (stl) xs[k * NX + jx] = yo;
         else us[k * NU + ju] = yo;
@@ -1069,7 +1115,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       ASTAMP(6);
     };
     if constexpr (!BOX) AS_WT(1);
-    for (int k0 = 0; k0 < N; k0 += FD) {
+    for (int k0 = 0; k0 < (REF ? 0 : N); k0 += FD) {
       static_for<FD>([&](auto s) {
         if (k0 + decltype(s)::value < N) stage(k0 + decltype(s)::value, s);
       });
@@ -1077,7 +1123,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     if constexpr (!BOX) AS_WT(2);
     // outputs of this pass: staged rows leave as 16-B vectors once the pass is known to be final
     // (the unconstrained pass; the active-set pass that converged or used the last iteration)
-    if (stage_out && stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
+    if (!REF && stage_out && stl) xs[N * NX + jx] = XU.at(N)[jx * SS] + zj;
     auto flush_out = [&]() {
       wave_lds_sync();
       constexpr int V = 16 / sizeof(T);
@@ -1157,7 +1203,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
           asm volatile("" ::"v"(acc));
         }
         RefIn<W32> in{a.x0 + b * a.x0_sb, XU, GP, ABT, KR, PS, cbase, cstride, refp, refs, xrN, W.QN,
-                      SW, PX, xs, us, us + N * NU,
+                      SW, PX, xs, us, us + N * NU, us + 2 * N * NU,
                       {crow[0], crow[1], crow[2], crow[3], crow[4], crow[5]},
                       lowm, upm, lbm, ubm, tol_u, N, iterate, ver};
         const RefOut<W32> ro = refine_verify<W32>(in);
@@ -1165,8 +1211,11 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         // release and re-fix alternate (a 2-cycle on 20 of 157 c4 instances: the exact multiplier
         // +1.7e-6, within the refinement's accuracy on fp32 data) stays at its bound, which moves
         // the solution by |mu| / s R ~ 1e-3 N at most
-        const M rd = rpass < REF_PASSES ? ro.rd : M(0), alo = ro.alo, ahi = ro.ahi;
+        // a component released and then found beyond its bound again is pinned at it (the 2-cycle)
+        const M rd = (rpass < REF_PASSES ? ro.rd : M(0)) & ~pin, alo = ro.alo, ahi = ro.ahi;
         ++rpass;
+        pin |= (alo | ahi) & relm;
+        relm |= rd;
 #if defined(MPCB_REF_TRACE) && defined(MPCB_AS_OWNER)   // (diagnostic builds: the passes of chunk instance MPCB_REF_TRACE)
         if (ver && c == MPCB_REF_TRACE && git < 128) {
           if (!stl) {
@@ -1177,7 +1226,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         }
 #endif
         if (ver) {
-          n_fwd += 6;
+          n_fwd += ro.sweeps;
           vlo = alo;
           vhi = ahi;
           vfl = rd & lowm;
@@ -1208,6 +1257,13 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     const M diff = stl ? M(0) : ((nlow ^ lowm) | (nup ^ upm));
     M changed = (bc<NX + 0>(diff) | bc<NX + 1>(diff)) | (bc<NX + 2>(diff) | bc<NX + 3>(diff));
     if (!done && !gconv) {
+      if constexpr (REF) {   // the refinement starts the next set from this point: fixed at the bounds
+        if (!stl) {
+          const M nf = (nlow | nup) & ~(lowm | upm);
+          for (int k = 0; k < N; ++k)
+            if ((nf >> k) & 1u) us[k * NU + ju] = ((nlow >> k) & 1u) ? lbm : ubm;
+        }
+      }
       lowm = nlow;
       upm = nup;
     } else {
@@ -1250,7 +1306,9 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
           int t = 0;
           if (j == 0) t = atomicAdd(a.as_ref, 1);
           t = bc<0>(t);
-          as_ref_put<W32>(a.as_ref + AS_REF_HDR + (int64_t)t * AS_REF_W, j, (int)c, git, n_fwd, n_bst, lowm, upm);
+          if (t < a.as_ref_cap)
+            as_ref_put<W32>(a.as_ref + AS_REF_HDR + (int64_t)t * AS_REF_W, j, (int)c, git, n_fwd, n_bst, lowm, upm);
+
         }
       }
       finish(!to_ipm);

@@ -48,7 +48,7 @@ as_ipm_kernel(SplitArgs<T> a) {
 
 template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
   unsigned g = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::box_elems<T>(a.N) * sizeof(T) : 0;
+  const size_t lds = a.N <= asq::OUT_NMAX ? (size_t)GROUPS * asq::out_elems<T>(a.N) * sizeof(T) : 0;
   if (a.as_queue && !dry_run()) {   // as many waves as stay resident; the rest of the chunk comes off the counter
     static const unsigned resident = [] {
       int dev = 0, cus = 0;
@@ -100,13 +100,14 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
         return (unsigned)cus * 4u * (unsigned)MPCB_AS_WAVES;
       }();
       unsigned gr = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+      const size_t lds_ref = (size_t)GROUPS * asq::ref_elems<float>(a.N) * sizeof(float);
       if (gr > resident_ref) gr = resident_ref;
       if (it) {
-        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true, true>), dim3(gr), dim3(64), lds, st, a);
-        else hipLaunchKernelGGL((as_ref_kernel_f32<false, true>), dim3(gr), dim3(64), lds, st, a);
+        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true, true>), dim3(gr), dim3(64), lds_ref, st, a);
+        else hipLaunchKernelGGL((as_ref_kernel_f32<false, true>), dim3(gr), dim3(64), lds_ref, st, a);
       } else {
-        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true>), dim3(gr), dim3(64), lds, st, a);
-        else hipLaunchKernelGGL((as_ref_kernel_f32<false>), dim3(gr), dim3(64), lds, st, a);
+        if (w32) hipLaunchKernelGGL((as_ref_kernel_f32<true>), dim3(gr), dim3(64), lds_ref, st, a);
+        else hipLaunchKernelGGL((as_ref_kernel_f32<false>), dim3(gr), dim3(64), lds_ref, st, a);
       }
     }
   }

@@ -95,6 +95,8 @@ struct mpcb_handle {
   int64_t params_count = 0;   // instance rows behind params (checked against B when params_sb != 0)
   int32_t* qp_stats = nullptr;   // 12/4 input box: per instance [forward passes, masked stages]
   int64_t qp_stats_rows = 0;     // instances of the last boxed solve
+  void* u_scratch = nullptr;     // fp32 12/4 input box: U when the caller passes none (the
+                                 // refinement kernel restarts from the active set's U, mpcb_as.h)
   const void* last_fn[LOG_SLOTS] = {};   // kernels the last solve launched (mpcb_last_kernels)
 };
 
@@ -289,6 +291,9 @@ static void select_path(mpcb_handle* h, const mpcb_config* cfg, int64_t max_batc
   h->scratch_bytes = h->chunk_elems * (int64_t)esz;
 }
 
+// the fp32 refinement list's capacity: 1/8 of the batch (c4 lists 252 of 65,536), at least 64
+static int64_t ref_cap(int64_t max_batch) { return max_batch / 8 > 64 ? max_batch / 8 : 64; }
+
 extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
   if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");
   *out = nullptr;
@@ -347,12 +352,15 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
   if (cfg->box_u && (full || h->split)) {
     // (+ 16: the 12/4 active-set kernel's work counter after the statistics; then its
     // interior-point fallback's list, 2 + max_batch: SplitArgs::as_fb; then the fp32 refinement
-    // list, AS_REF_HDR + AS_REF_W max_batch: SplitArgs::as_ref)
+    // list, AS_REF_HDR + AS_REF_W ref_cap(max_batch): SplitArgs::as_ref)
     e = hipMalloc((void**)&h->qp_stats,
-                  ((size_t)max_batch * (3 + AS_REF_W) + 18 + AS_REF_HDR) * sizeof(int32_t));
+                  ((size_t)max_batch * 3 + 18 + AS_REF_HDR + (size_t)AS_REF_W * ref_cap(max_batch)) * sizeof(int32_t));
+    if (e == hipSuccess && !full && cfg->dtype == MPCB_F32)
+      e = hipMalloc(&h->u_scratch, (size_t)max_batch * cfg->N * 4 * sizeof(float));
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
       (void)hipFree(h->weights);
+      if (h->qp_stats) (void)hipFree(h->qp_stats);
       delete h;
       return fail(MPCB_E_NOMEM, "qp stats: %s", hipGetErrorString(e));
     }
@@ -370,6 +378,7 @@ extern "C" int mpcb_destroy(mpcb_handle* h) {
   (void)hipFree(h->scratch);
   (void)hipFree(h->weights);
   if (h->qp_stats) (void)hipFree(h->qp_stats);
+  if (h->u_scratch) (void)hipFree(h->u_scratch);
   delete h;
   return MPCB_OK;
 }
@@ -496,6 +505,8 @@ static int solve_body(mpcb_handle* h, int64_t B, int mode, const void* x0, int64
       a.as_fb = (h->cfg.box_u && h->qp_stats) ? h->qp_stats + 2 * h->max_batch + 16 : nullptr;
       a.as_ref = (sizeof(T) == 4 && h->cfg.box_u && h->qp_stats) ? h->qp_stats + 3 * h->max_batch + 18 : nullptr;
       if (const char* e = getenv("MPCB_AS_REFINE")) if (atoi(e) == 0) a.as_ref = nullptr;   // (A/B: no refinement)
+      a.as_ref_cap = (int)ref_cap(h->max_batch);
+      if (a.as_ref && !a.U) a.U = (T*)h->u_scratch;   // (the refinement kernel restarts from U)
       a.as_order = (h->cfg.box_u && b0 == 0) ? h->as_order_dbg : nullptr;
       hipEvent_t* ev = (h->timing && chunk_i < mpcb_handle::TCHUNKS) ? h->ev[chunk_i] : nullptr;
       hipError_t e = launch_split<T>(a, (hipStream_t)stream, ev);

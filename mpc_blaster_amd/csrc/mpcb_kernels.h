@@ -162,6 +162,7 @@ struct SplitArgs {
                      // chunk instance), filled by the active-set kernel (mpcb_asipm.h)
   int* as_ref;       // fp32 box path (nullable): the refinement list (mpcb_as.h AS_REF_*), filled by
                      // the active-set kernel, walked by the refinement kernel
+  int as_ref_cap;    // entries the refinement list holds
   int max_as_iter;
   int small;         // 1: small unconstrained chunk: parallel linearisation + cached-[A|B] passes
   int fwd16;         // 1: P2 exports [A|B]^T and the forward pass runs in the 16-lane layout
