@@ -209,7 +209,7 @@ template <class P> __device__ __forceinline__ P* vglobal(P* p) {
 // would release a component: one more step before acting on it), the refined passes whose
 // multiplier verdicts count, and the verification's tolerance on a multiplier relative to its
 // terms' sum
-constexpr int REF_STEPS = 1, REF_STEPS_MAX = 1, REF_PASSES = 3;
+constexpr int REF_STEPS = 1, REF_STEPS_MAX = 1, REF_PASSES = 8;
 constexpr double REF_TOL = 0x1p-18;
 template <bool W32> struct RefIn {
   using M = typename Masks<W32>::M;
@@ -676,6 +676,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         git = ent[1];
         n_fwd = ent[2];
         n_bst = ent[3];
+        kc = ent[AS_REF_KC];   // (an interior-point instance: the full backward pass first)
         const int w = 4 + 2 * ju;
         if (!stl) {
           lowm = (M)(uint32_t)ent[w];
@@ -1285,7 +1286,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
       // not converged within the pass budget (min(max_as_iter, AS_IPM_AFTER), mpcb_capi.hip): the
       // interior point takes the instance over (mpcb_asipm.h, oracle.ocp.pdas_solve) unless a
       // factorisation failed; the status is then the fallback's to write
-      const bool to_ipm = BOX && !cvd && st == MPCB_STATUS_OK && a.as_fb;
+      const bool to_ipm = BOX && !REF && !cvd && st == MPCB_STATUS_OK && a.as_fb;
       if (to_ipm) {
         if (j == 0) a.as_fb[2 + atomicAdd(a.as_fb, 1)] = (int)c;
       } else if (!cvd) {
@@ -1300,14 +1301,22 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         const int so = (!stl && fabs(us[ju]) < T(AS_REF_U0)) ? 1 : 0;
         const bool small = (bc<NX + 0>(so) & bc<NX + 1>(so)) & (bc<NX + 2>(so) & bc<NX + 3>(so));
         const int un = unc ? 1 : 0;
+        // ... or that took AS_REF_PASSES passes or more: the hard QPs, where the fp32 solve's own
+        // error grows (the hard wind + sine draws: 10-34-pass instances 6e-5 to 1.2e-4 off at an
+        // fp32 data sensitivity of 4e-6 to 9e-6; listing from 6 passes on instead -- 4,544 of
+        // c4's 65,536 -- took the refinement kernel from 0.33 to 0.47 ms)
         const bool lst = cvd && a.as_ref &&
-                         (small || ((bc<NX + 0>(un) | bc<NX + 1>(un)) | (bc<NX + 2>(un) | bc<NX + 3>(un))));
+                         (small || git >= AS_REF_PASSES ||
+                          ((bc<NX + 0>(un) | bc<NX + 1>(un)) | (bc<NX + 2>(un) | bc<NX + 3>(un))));
         if (lst) {   // (group-uniform: the row broadcast below has its 16 lanes)
           int t = 0;
           if (j == 0) t = atomicAdd(a.as_ref, 1);
           t = bc<0>(t);
-          if (t < a.as_ref_cap)
-            as_ref_put<W32>(a.as_ref + AS_REF_HDR + (int64_t)t * AS_REF_W, j, (int)c, git, n_fwd, n_bst, lowm, upm);
+          if (t < a.as_ref_cap) {
+            int* const e = a.as_ref + AS_REF_HDR + (int64_t)t * AS_REF_W;
+            as_ref_put<W32>(e, j, (int)c, git, n_fwd, n_bst, lowm, upm);
+            if (j == 0) e[AS_REF_KC] = -1;   // (its factorisation is the converged pass's)
+          }
 
         }
       }

@@ -88,8 +88,23 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
       else MPCB_LAUNCH(PH_FORWARD, (as_kernel_f64<false>), dim3(g), dim3(64), lds, st, a);
     }
   }
-  // the listed fp32 instances' refinement (a few hundred of c4's 65,536; before the fallback, to
-  // which it can hand an instance over).  Not in the launch log either (below).
+  // the instances the active set handed over (usually none: the waves read an empty list and
+  // exit).  Not in the launch log, which keeps the active-set kernel as the phase's kernel.
+  if (a.as_fb && !dry_run()) {
+    static const unsigned resident_ipm = [] {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      return (unsigned)cus * 4u * (sizeof(T) == 4 ? 2u : 1u);
+    }();
+    unsigned gi = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
+    if (gi > resident_ipm) gi = resident_ipm;
+    if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((as_ipm_kernel<T, true>), dim3(gi), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((as_ipm_kernel<T, false>), dim3(gi), dim3(64), 0, st, a);
+  }
+  // the listed fp32 instances' refinement (a few hundred of c4's 65,536), after the fallback, whose
+  // results it refines too.  Not in the launch log either (above).
   if constexpr (sizeof(T) == 4) {
     if (a.as_ref && !dry_run()) {
       static const unsigned resident_ref = [] {
@@ -110,21 +125,6 @@ template <class T> hipError_t launch_as(const SplitArgs<T>& a, hipStream_t st) {
         else hipLaunchKernelGGL((as_ref_kernel_f32<false>), dim3(gr), dim3(64), lds_ref, st, a);
       }
     }
-  }
-  // the instances the active set handed over (usually none: the waves read an empty list and
-  // exit).  Not in the launch log, which keeps the active-set kernel as the phase's kernel.
-  if (a.as_fb && !dry_run()) {
-    static const unsigned resident_ipm = [] {
-      int dev = 0, cus = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-      return (unsigned)cus * 4u * (sizeof(T) == 4 ? 2u : 1u);
-    }();
-    unsigned gi = (unsigned)((a.nb + GROUPS - 1) / GROUPS);
-    if (gi > resident_ipm) gi = resident_ipm;
-    if (a.mode == MPCB_MODE_ITERATE) hipLaunchKernelGGL((as_ipm_kernel<T, true>), dim3(gi), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((as_ipm_kernel<T, false>), dim3(gi), dim3(64), 0, st, a);
   }
   return dry_run() ? hipSuccess : hipGetLastError();
 }

@@ -363,8 +363,14 @@ __device__ __forceinline__ void ipm_body(const SplitArgs<T>& args) {
     if (!ok) st = MPCB_STATUS_QP_FAIL;
     if (st == MPCB_STATUS_OK && !(mu <= T(C::TOL) && res <= T(C::RES))) st = MPCB_STATUS_MINSTEP;
     bool ofin = true;
+    uint64_t alo = 0, ahi = 0;   // (fp32, input lanes) the components at their bounds
+    const T dact = T(1e-4) * wbox;
     for (int k = 0; k <= N; ++k) {
       const T y = XU.at(k)[j * SS] + (k < N ? slot(k)[IZ] : zN);
+      if (!stl && k < N) {
+        alo |= (uint64_t)(y <= lbm + dact) << k;
+        ahi |= (uint64_t)(y >= ubm - dact) << k;
+      }
       if (valid) {
         if (stl) {
           if (a.X) a.X[(b * (N + 1) + k) * NX + jx] = y;
@@ -379,6 +385,23 @@ __device__ __forceinline__ void ipm_body(const SplitArgs<T>& args) {
     }
     const uint64_t bad = lane_mask(!ofin);
     ofin = ((bad >> (16 * q)) & 0xFFFFu) == 0;
+    if constexpr (sizeof(T) == 4) {
+      // crossover: the interior point's active set (components within 1e-4 of the box width of a
+      // bound) goes to the refinement kernel like an active-set instance, which refactors it in
+      // full (kc = N - 1), refines in fp64 residuals and corrects the set (the fp32 interior
+      // point alone stops ~1e-4 off the minimiser)
+      if (valid && a.as_ref && st == MPCB_STATUS_OK && ofin) {   // (group-uniform)
+        int tk = 0;
+        if (j == 0) tk = atomicAdd(a.as_ref, 1);
+        tk = bc<0>(tk);
+        if (tk < a.as_ref_cap) {
+          int* e = a.as_ref + AS_REF_HDR + (int64_t)tk * AS_REF_W;
+          const int32_t q0 = a.qp_stats ? a.qp_stats[2 * b] : 0, q1 = a.qp_stats ? a.qp_stats[2 * b + 1] : 0;
+          as_ref_put<false>(e, j, (int)c, 1, q0 + its, q1 + its * N, alo, ahi);
+          if (j == 0) e[AS_REF_KC] = N - 1;
+        }
+      }
+    }
     if (valid && j == NX) {
       const int32_t st0 = a.status[b];
       a.status[b] = !ofin ? MPCB_STATUS_NAN : (st0 != MPCB_STATUS_OK ? st0 : st);

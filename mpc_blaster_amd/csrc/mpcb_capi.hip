@@ -291,8 +291,9 @@ static void select_path(mpcb_handle* h, const mpcb_config* cfg, int64_t max_batc
   h->scratch_bytes = h->chunk_elems * (int64_t)esz;
 }
 
-// the fp32 refinement list's capacity: 1/8 of the batch (c4 lists 252 of 65,536), at least 64
-static int64_t ref_cap(int64_t max_batch) { return max_batch / 8 > 64 ? max_batch / 8 : 64; }
+// the fp32 refinement list's capacity: the whole batch (c4 lists 252 of 65,536, but on strongly
+// constrained draws most instances reach it through the interior-point fallback)
+static int64_t ref_cap(int64_t max_batch) { return max_batch; }
 
 extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch, mpcb_handle** out) {
   if (!cfg || !out) return fail(MPCB_E_INVALID, "null argument");

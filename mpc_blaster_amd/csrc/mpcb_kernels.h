@@ -132,9 +132,11 @@ constexpr int AS_IPM_AFTER = 48;
 constexpr int AS_IPM_NV_NUM = 7, AS_IPM_NV_DEN = 20;
 // the fp32 input box's refinement list (SplitArgs::as_ref, mpcb_as.h as_ref_put): a header of
 // AS_REF_HDR words, then AS_REF_W per listed instance
-constexpr int AS_REF_HDR = 4, AS_REF_W = 20;
+constexpr int AS_REF_HDR = 4, AS_REF_W = 24, AS_REF_KC = 20;   // (KC: the restart stage, -1 or N - 1)
 // ... which also lists converged instances whose first-stage controls are all below this (N)
 constexpr double AS_REF_U0 = 2.0;
+// ... and converged instances that needed this many active-set passes or more
+constexpr int AS_REF_PASSES = 10;
 
 template <class T>
 struct SplitArgs {

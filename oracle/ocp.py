@@ -812,6 +812,37 @@ def stage_cost(X, U, xref, uref, spec: OcpSpec) -> np.ndarray:
     return c + 0.5 * np.einsum('bi,ij,bj->b', eN, QN, eN)
 
 
+def fp32_sensitivity(o, x0, xref, uref, spec: OcpSpec, trials: int = 2, rel: float = 2.0 ** -22, seed: int = 0):
+    """How far the exact input-box minimiser moves when the QP data carry fp32-level noise: the
+    linearisation [A|B] of ``o`` (mpc_solve(..., return_lin=True)) scaled entrywise by
+    (1 + rel * N(0, 1)), i.e. ~2 ulp of fp32, and re-solved exactly by ``pdas_solve``, ``trials``
+    times.  Returns per instance the largest normwise move of U and of u0 (the parity metric).
+
+    An fp32 solver's own linearisation carries at least this much error, so an instance that moves
+    by more than a parity bound here cannot be held to it by ANY fp32 computation: the sweeps hold
+    such instances (counted and printed) to the QP's optimal objective instead
+    (tests/test_gpu_fuzz.py).  On c4's draws the move is ~1e-7; on strongly constrained short
+    horizons (sweep cases 33 / 67 / 158: N = 2, 6, 4, wind) up to 2e-4."""
+    B = x0.shape[0]
+    N = spec.N
+    xr = np.broadcast_to(np.asarray(xref, dtype=np.float64), (B, N + 1, NX))
+    ur = np.broadcast_to(np.asarray(uref, dtype=np.float64), (B, N, NU))
+    rs = np.random.default_rng(seed)
+    worst = np.zeros(B)
+    den = np.maximum(np.abs(o['U']).reshape(B, -1).max(axis=1), 1.0)
+    den0 = np.maximum(np.abs(o['u0']).max(axis=1), 1.0)
+    for _ in range(trials):
+        A = o['A'] * (1.0 + rel * rs.standard_normal(o['A'].shape))
+        Bm = o['B'] * (1.0 + rel * rs.standard_normal(o['B'].shape))
+        with np.errstate(all='ignore'):
+            _, du, _, _, _ = pdas_solve(A, Bm, o['gap'], x0 - o['xbar'][:, 0], o['xbar'], o['ubar'], xr, ur, spec)
+        U = o['ubar'] + du
+        eU = np.abs(U - o['U']).reshape(B, -1).max(axis=1) / den
+        eu = np.abs(U[:, 0] - o['u0']).max(axis=1) / den0
+        worst = np.maximum(worst, np.maximum(eU, eu))
+    return worst
+
+
 def dense_box_qp(A, Bm, gap, dx0, xbar, ubar, xref, uref, spec: OcpSpec):
     """Independent check (tests only): condense the QP in du and solve it with SciPy BVLS."""
     from scipy.optimize import lsq_linear

@@ -171,9 +171,11 @@ def test_box_slow_instances_take_the_interior_point(dtype, mode):
     """The 12/4 input box's fallback (mpcb_asipm.h): on draws where the active set's backup rule is
     slow (sine references, +-5 N wind) the instances unconverged after AS_IPM_AFTER passes are
     solved by the interior point, as in oracle.ocp.pdas_solve.  fp64: the device against the oracle
-    at 1e-9 normwise, same statuses (all OK).  fp32: its interior point stops at mu <= 1e-6 (the
-    17/6 fp32 tolerances), so it is checked against the fp64 oracle at 5e-4 normwise, inside the
-    box."""
+    at 1e-9 normwise, same statuses (all OK).  fp32: the interior point stops at mu <= 1e-8
+    (IpmTol<float>) about 1e-4 off the minimiser, and its active set then goes through the
+    refinement kernel (crossover, mpcb_asipm.h), so every instance that fp32 data can pin
+    (oracle.ocp.fp32_sensitivity <= 1e-5) is held to 5e-5 normwise, the others (counted) to the
+    QP's optimal objective; all inside the box."""
     from test_oracle_ocp import hard_box_inputs
     from oracle.ocp import AS_IPM_AFTER
     N, B = 18, 192
@@ -198,8 +200,20 @@ def test_box_slow_instances_take_the_interior_point(dtype, mode):
           f'after {AS_IPM_AFTER} passes), max rel err {e:.2e}, status {np.bincount(st, minlength=5).tolist()}')
     assert fb.sum() >= 5
     assert (st == 0).all() and (o['status'] == 0).all()
-    assert e < (1e-9 if dtype == 'f64' else 5e-4)
-    tb = 1e-7 if dtype == 'f64' else 1e-4   # (interior iterates; fp32: its residual bound 1e-5)
+    if dtype == 'f64':
+        assert e < 1e-9
+    else:
+        from oracle.ocp import fp32_sensitivity
+        from test_gpu_fuzz import qp_objective
+        o = mpc_solve(x0, xref, uref, spec, wind=wind, return_lin=True,
+                      **(dict(mode='iterate', xbar=xbar, ubar=ubar) if mode == 'iterate' else {}))
+        ill = fp32_sensitivity(o, x0, xref, uref, spec) > 1e-5
+        ew = max(relerr(u0, o['u0'])[~ill].max(), relerr(X, o['X'])[~ill].max(), relerr(U, o['U'])[~ill].max())
+        gap = qp_objective(o, U, x0, xref, uref, spec) / np.abs(qp_objective(o, o['U'], x0, xref, uref, spec)) - 1.0
+        print(f'  fp32: {int(ill.sum())} of {B} fp32-ill-conditioned; the others max rel err {ew:.2e}; '
+              f'objective gap max {gap.max():.2e}')
+        assert ew < 5e-5 and (gap < 1e-5).all()
+    tb = 1e-7 if dtype == 'f64' else 2e-4   # (interior iterates; fp32: the violation tolerance tol_u)
     assert (U >= -tb).all() and (U <= 65 + tb).all()
 
 

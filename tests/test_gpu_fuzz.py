@@ -9,12 +9,14 @@ everywhere and on X, U up to N = 40 (the BASELINE horizons); beyond that the fp3
 rollout that rollout mode linearises at drifts from the fp64 one, and X, U with it, roughly as N^2
 (measured 6e-5 at N = 56, 1.4e-4 at 80, 3.1e-4 at 105; iterate mode, which takes the iterate as
 given, stays near 1e-5 at N = 108; the small-chunk path reached 2.6e-4 at N = 89), so the X / U
-bound is 1e-4 (N / 40)^2 there.  fp32 instances
-fp32 box cases are held to optimality instead of to the fp64 minimiser: the QP objective of the
-device's U (states by the oracle's linearised dynamics) within 1e-5 of the oracle's optimum, u0
-within 2e-2, U inside the box up to the active set's fp32 violation tolerance (1.3e-4).  Along nearly flat directions of strongly constrained QPs the fp32 active set and the
-fp32 interior point alike land up to ~1e-2 off the minimiser at an objective within ~1e-6 (the
-sweeps of cases 0-247, profiles/r05/gpu_fuzz_b29_128.log and gpu_fuzz_b36_128_248.log).
+bound is 1e-4 (N / 40)^2 there.  The fp32 input box is held to the same bounds, except on the
+instances whose exact minimiser itself moves by more than 1e-5 when [A|B] carries ~2 ulp of fp32
+noise (oracle.ocp.fp32_sensitivity: no fp32 linearisation can pin those, e.g. 20 of case 158's 447,
+N = 4 with wind); those are counted, printed and held to the QP's optimal objective (within 1e-5)
+instead.  Of the others, at most 1 % of a case's instances may exceed the bound (all within 1e-3;
+counted and printed): strongly constrained draws where neither the active set's refinement nor the
+interior point's crossover reaches the exact set (profiles/r06/fuzz_box32.log).  Before the fp64-residual refinement (mpcb_as.h refine_verify) the fp32 box cases were
+up to 1e-2 off in u0 (profiles/r05/gpu_fuzz_b36_128_248.log); after it, profiles/r06/fuzz_box32.log.
 """
 import os
 
@@ -22,7 +24,7 @@ import numpy as np
 import pytest
 
 from oracle.inputs import make_inputs
-from oracle.ocp import OcpSpec, mpc_solve
+from oracle.ocp import OcpSpec, fp32_sensitivity, mpc_solve
 
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
@@ -119,12 +121,25 @@ def test_random_config_matches_oracle(case, monkeypatch):
         txu = 5e-5 if N <= 40 else 1e-4 * (N / 40) ** 2
         assert (eu < 5e-5).all() and (ex < txu).all() and (eU < txu).all()
     else:
-        # fp32 box QPs: held to optimality, not to the fp64 minimiser -- along nearly flat
-        # directions of strongly constrained QPs fp32 lands up to ~4e-3 off the minimiser with
-        # the objective within ~1e-6 of the optimum
+        # fp32 box: the bounds above on every instance that fp32 data can pin (module docstring);
+        # the others (fp32_sensitivity > 1e-5) to the QP's optimal objective
+        sens = fp32_sensitivity(o, x0, xref, uref, spec)
+        ill = sens > 1e-5
+        txu = 5e-5 if N <= 40 else 1e-4 * (N / 40) ** 2
         gap = qp_objective(o, U, x0, xref, uref, spec) / np.abs(qp_objective(o, o['U'], x0, xref, uref, spec)) - 1.0
-        print(f'  fp32 box: objective gap max {gap.max():.2e}, u0 {eu.max():.2e}')
-        assert (gap < 1e-5).all() and (eu < 2e-2).all()
+        wc = ~ill
+        over = wc & ((eu >= 5e-5) | (ex >= txu) | (eU >= txu))
+        worst = np.maximum(np.maximum(eu, ex), eU)
+        print(f'  fp32 box: {int(ill.sum())} of {B} instances fp32-ill-conditioned (sensitivity max '
+              f'{sens.max():.1e}); the others: u0 {eu[wc].max(initial=0):.2e} X {ex[wc].max(initial=0):.2e} '
+              f'U {eU[wc].max(initial=0):.2e}, {int(over.sum())} beyond the bound '
+              f'({int((over & o["fallback"]).sum())} of them through the interior point); objective gap max {gap.max():.2e}')
+        # measured over cases 0-247 (profiles/r06/fuzz_box32.log): at most 1 % of a case's
+        # well-conditioned instances beyond the bound, none beyond 6.2e-4 -- strongly constrained
+        # short horizons and the interior point's hand-overs, whose refinement does not always
+        # reach the exact set
+        assert over.sum() <= max(1, B // 100) and (worst[wc] < 1e-3).all()
+        assert (gap < 1e-5).all()
     if box:   # (fp32: the active set's violation tolerance 16 eps (|lb| + |ub| + 1) = 1.3e-4)
         tb = 1e-6 if dtype == 'f64' else 2e-4
         assert (U >= -tb).all() and (U <= 65 + tb).all()
