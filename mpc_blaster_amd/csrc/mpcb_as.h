@@ -157,9 +157,9 @@ template <class T> __device__ __forceinline__ Arr<T> arr2(T* base, int rec, int6
 constexpr int OUT_NMAX = 64;   // longer horizons store directly
 template <class T> __host__ __device__ constexpr int out_elems(int N) { return (N + 1) * NX + N * NU; }
 // the refinement kernel's block per instance: the staged rows, then the refinement's N x NU
-// feedforward terms and (N + 1) x NX state errors x - xref
+// feedforward terms and (N + 1) x NX state errors x - xref, then a copy of the staged U and X rows
 template <class T> __host__ __device__ constexpr int ref_elems(int N) {
-  return out_elems<T>(N) + N * NU + (N + 1) * NX;
+  return 2 * out_elems<T>(N) + N * NU + (N + 1) * NX;   // (+ a copy of the staged rows)
 }
 
 // Stage masks (active sets, violations: bit k = stage k) of a horizon N <= 32 in 32-bit registers
@@ -662,11 +662,12 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
   int git = 0;                  // passes of the group's current instance
   int rpass = 0;                // REF: refined passes of the group's current instance
   M relm = 0, pin = 0;          // REF, input lanes: stages released by the refinement; fixed again after
+  M lrel = 0;                   // REF, input lanes: the releases the last refined pass applied
   // REF: the listed instance's active set and counts (as_ref_put), and its U (the output the
   // active-set kernel wrote: mpcb_solve passes a U buffer of the handle's when the caller has none)
   auto restore = [&]() {
     rpass = 0;
-    relm = pin = 0;
+    relm = pin = lrel = 0;
     if constexpr (REF) {
       if (valid) {
         T* const us0 = reinterpret_cast<T*>(as_dyn) + q * ref_elems<T>(N) + (N + 1) * NX;
@@ -1217,6 +1218,32 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         ++rpass;
         pin |= (alo | ahi) & relm;
         relm |= rd;
+        // the previous pass's releases all came back (beyond their bounds) and nothing else
+        // changed: the set is the one before them, whose refined rows were kept -- finish with
+        // those instead of refactoring the set once more (the slowest c4 instances' third pass)
+        {
+          T* const ubk = us + 2 * N * NU + (N + 1) * NX;
+          T* const xbk = ubk + N * NU;
+          const int mine = (stl || (rd == 0 && (alo | ahi) == lrel)) ? 1 : 0;
+          const int anyr = (!stl && lrel != 0) ? 1 : 0;
+          const bool undo = ((bc<NX + 0>(mine) & bc<NX + 1>(mine)) & (bc<NX + 2>(mine) & bc<NX + 3>(mine))) &&
+                            ((bc<NX + 0>(anyr) | bc<NX + 1>(anyr)) | (bc<NX + 2>(anyr) | bc<NX + 3>(anyr)));
+          const int rel_o = (!stl && rd != 0) ? 1 : 0;
+          const bool releases = (bc<NX + 0>(rel_o) | bc<NX + 1>(rel_o)) | (bc<NX + 2>(rel_o) | bc<NX + 3>(rel_o));
+          wave_lds_sync();
+          if (ver && undo) {
+            for (int e = j; e < N * NU; e += NZ) us[e] = ubk[e];
+            for (int e = j; e < (N + 1) * NX; e += NZ) xs[e] = xbk[e];
+            lowm |= alo;
+            upm |= ahi;
+          } else if (ver && releases) {
+            for (int e = j; e < N * NU; e += NZ) ubk[e] = us[e];
+            for (int e = j; e < (N + 1) * NX; e += NZ) xbk[e] = xs[e];
+          }
+          wave_lds_sync();
+          lrel = (ver && releases && !undo) ? rd : M(0);
+          if (ver && undo) rpass = -1;   // (marker: converged by the undo, below)
+        }
 #if defined(MPCB_REF_TRACE) && defined(MPCB_AS_OWNER)   // (diagnostic builds: the passes of chunk instance MPCB_REF_TRACE)
         if (ver && c == MPCB_REF_TRACE && git < 128) {
           if (!stl) {
@@ -1228,10 +1255,12 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
 #endif
         if (ver) {
           n_fwd += ro.sweeps;
-          vlo = alo;
-          vhi = ahi;
-          vfl = rd & lowm;
-          vfu = rd & upm;
+          const bool und = rpass < 0;
+          if (und) rpass = REF_PASSES;
+          vlo = und ? M(0) : alo;
+          vhi = und ? M(0) : ahi;
+          vfl = und ? M(0) : rd & lowm;
+          vfu = und ? M(0) : rd & upm;
         }
       }
     }
