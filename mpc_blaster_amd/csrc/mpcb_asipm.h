@@ -279,7 +279,7 @@ __device__ __forceinline__ void ipm_body(const SplitArgs<T>& args) {
         fin = ((bad_fin >> (16 * q)) & 0xFFFFu) == 0;
         qp_ok = ((bad_qp >> (16 * q)) & 0xFFFFu) == 0;
       }
-      ok = ok && (fin || !valid);
+      ok = ok && (fin || !valid || !act);   // (a finished group's recomputed pass is not its verdict)
       act = act && fin;
       const bool brk = !qp_ok && act && mu <= T(C::BREAK) && res <= T(C::RES);
       conv = conv || brk;

@@ -176,3 +176,33 @@ def mpc_solve17(x0, xref, uref, spec: FullSpec, p25=None, mode='rollout', xbar=N
     status = np.where(bad, STATUS_NAN, status).astype(np.int32)
     return dict(u0=U[:, 0].copy(), X=X, U=U, status=status, iters=iters, xbar=xbar, ubar=ubar,
                 A=A, B=Bm, gap=gap)
+
+
+def sensitivity17(o, x0, xref, uref, spec: FullSpec, rel: float, trials: int = 1, seed: int = 0):
+    """How far the exact boxed minimiser of the 17/6 OCP moves when its linearisation [A|B] (of
+    ``o`` = mpc_solve17(...)) carries relative noise ``rel`` (2^-45: a few fp64 ulp; 2^-22: fp32):
+    re-solved by the same interior point + polish, per instance the largest normwise move of U and
+    of u0 (oracle.ocp.fp32_sensitivity's 17/6 counterpart; test infrastructure only).  An instance
+    that moves by more than a parity bound under noise its arithmetic carries anyway is degenerate
+    for that bound (a flat direction of a strongly constrained QP): tests/test_gpu_fuzz17.py counts
+    such instances and holds them to the optimal objective."""
+    x0 = np.asarray(x0, dtype=np.float64)
+    Bsz, N = x0.shape[0], spec.N
+    xr = np.broadcast_to(np.asarray(xref, dtype=np.float64), (Bsz, N + 1, NX17))
+    ur = np.broadcast_to(np.asarray(uref, dtype=np.float64), (Bsz, N, NU17))
+    rs = np.random.default_rng(seed)
+    den = np.maximum(np.abs(o['U']).reshape(Bsz, -1).max(axis=1), 1.0)
+    den0 = np.maximum(np.abs(o['u0']).max(axis=1), 1.0)
+    worst = np.zeros(Bsz)
+    for _ in range(trials):
+        A = o['A'] * (1.0 + rel * rs.standard_normal(o['A'].shape))
+        Bm = o['B'] * (1.0 + rel * rs.standard_normal(o['B'].shape))
+        with np.errstate(all='ignore'):
+            _, du, st, _ = ipm_box_solve(A, Bm, o['gap'], x0 - o['xbar'][:, 0], o['xbar'], o['ubar'], xr, ur, spec,
+                                         max_iter=spec.max_as_iter, lbx=spec.lbx, ubx=spec.ubx)
+        U = o['ubar'] + du
+        mv = np.maximum(np.abs(U - o['U']).reshape(Bsz, -1).max(axis=1) / den,
+                        np.abs(U[:, 0] - o['u0']).max(axis=1) / den0)
+        worst = np.maximum(worst, np.where(st == STATUS_OK, mv, np.inf))
+    return worst
+

@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle.full import FullSpec, default_p25, mpc_solve17
+from oracle.full import FullSpec, default_p25, mpc_solve17, sensitivity17
 
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
@@ -143,19 +143,35 @@ def test_random_full17_config_matches_oracle(case):
     emax = max(relerr(u0, o['u0'])[ok].max(initial=0), relerr(X, o['X'])[ok].max(initial=0),
                relerr(U, o['U'])[ok].max(initial=0))
     if dtype == 'f64':
-        # same statuses, except that the state box's polish may certify an instance on one side
-        # and leave it at the interior point's conditioning limit (MINSTEP) on the other
+        # same statuses, except that the state box's polish may certify ONE instance on one side and
+        # leave it at the interior point's conditioning limit (MINSTEP) on the other (1 of 57 in
+        # case 66 of the 128-case sweep)
         diff = st != o['status']
         minstep = {0, MINSTEP}
         assert all({int(a), int(b)} <= minstep for a, b in zip(st[diff], o['status'][diff]))
-        assert diff.sum() <= max(1, B // 20)
+        assert diff.sum() <= 1
         if c['bounds'] == 'none':
             assert emax <= 1e-9
-        else:   # optimal and feasible as the oracle's; the minimiser itself within 1e-5
-            assert jgap[ok].max(initial=0) <= 1e-9 and vd[ok].max(initial=0) <= 1e-9 and emax <= 1e-5
+        else:
+            # optimal and feasible as the oracle's; the minimiser within 1e-8 on every instance
+            # that is not degenerate at fp64 precision (its exact minimiser moves by more than
+            # 1e-9 under a few ulp of noise on [A|B], oracle.full.sensitivity17: a flat direction)
+            flat = sensitivity17(o, x0, xref, uref, spec, rel=2.0 ** -45) > 1e-9
+            w = ok & ~flat
+            ew = max(relerr(u0, o['u0'])[w].max(initial=0), relerr(X, o['X'])[w].max(initial=0),
+                     relerr(U, o['U'])[w].max(initial=0))
+            print(f'  fp64 boxed: {int((ok & flat).sum())} of {int(ok.sum())} degenerate; the others within {ew:.1e}')
+            assert jgap[ok].max(initial=0) <= 1e-9 and vd[ok].max(initial=0) <= 1e-9 and ew <= 1e-8
     else:
         assert (st == 0).all()
         if c['bounds'] == 'none':
             assert e[0] <= 5e-3
         else:
+            # the input box in fp32: held to the optimal objective; u0 against the fp64 minimiser
+            # is reported with the instances' fp32 sensitivity (the measured reason it can be far)
+            sens = sensitivity17(o, x0, xref, uref, spec, rel=2.0 ** -22)
+            eu = relerr(u0, o['u0'])
+            pin = sens <= 1e-5
+            print(f'  fp32 boxed: u0 max {eu.max():.1e}; fp32 sensitivity max {sens.max():.1e}; '
+                  f'u0 on the {int(pin.sum())} fp32-pinnable instances {eu[pin].max(initial=0):.1e}')
             assert jgap.max() <= 1e-5
