@@ -226,6 +226,13 @@ def run(w, world, rank, dev, steps, warmup, stub=None, dump_gather=None):
         st = mpc.qp_stats(B).double().cpu().numpy()
         qp = dict(fwd_passes=float(st[:, 0].sum()), bwd_stages=float(st[:, 1].sum()),
                   mean_iters=float(st[:, 0].mean()), max_iters=int(st[:, 0].max()))
+        if cuda and w['dtype'] == 'f32' and hasattr(getattr(mpc, 'lib', None), 'mpcb_debug_ref_list'):
+            # instances the fp32 refinement kernel took (last chunk): its sweeps are counted in
+            # fwd_passes / bwd_stages and its time in the phase, next to as_kernel's own
+            import ctypes
+            rl = (ctypes.c_int32 * 2)()
+            if mpc.lib.mpcb_debug_ref_list(mpc._h, rl) == 0:
+                qp['refined_last_chunk'] = int(rl[0])
         if world > 1:
             t = torch.tensor([qp['fwd_passes'], qp['bwd_stages']], dtype=torch.float64, device=odev)
             dist.all_reduce(t)
@@ -388,6 +395,12 @@ def summarize(w, r, world, steps):
         gbs = byt / (ph[dom] * 1e-3) / 1e9
         roof.update(bound='hbm', achieved=gbs, peak=HBM_PEAK_GBS, unit='GB/s', frac=gbs / HBM_PEAK_GBS,
                     bytes_per_phase=byt,
+                    phase_note=('the forward phase (HIP events around it) holds as_kernel plus the '
+                                'input-box hand-overs launched after it on the same stream: the '
+                                'interior-point fallback (as_ipm_kernel) and the fp32 refinement '
+                                '(as_ref_kernel_f32, active_set.refined_last_chunk instances); '
+                                'their passes are in active_set.fwd_passes / bwd_stages, and '
+                                'traffic / executed flops are as_kernel\'s own PMC entry'),
                     traffic_frac=(tr / (ph[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS) if tr else None)
     return value, roof
 

@@ -358,6 +358,7 @@ extern "C" int mpcb_create(const mpcb_config* cfg, int device, int64_t max_batch
                   ((size_t)max_batch * 3 + 18 + AS_REF_HDR + (size_t)AS_REF_W * ref_cap(max_batch)) * sizeof(int32_t));
     if (e == hipSuccess && !full && cfg->dtype == MPCB_F32)
       e = hipMalloc(&h->u_scratch, (size_t)max_batch * cfg->N * 4 * sizeof(float));
+    if (h->u_scratch) h->scratch_bytes += (int64_t)max_batch * cfg->N * 4 * sizeof(float);
     if (e != hipSuccess) {
       (void)hipFree(h->scratch);
       (void)hipFree(h->weights);

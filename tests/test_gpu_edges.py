@@ -217,6 +217,41 @@ def test_box_slow_instances_take_the_interior_point(dtype, mode):
     assert (U >= -tb).all() and (U <= 65 + tb).all()
 
 
+@pytest.mark.parametrize('dtype', ['f64', 'f32'])
+def test_box_fallback_and_refinement_are_order_and_run_invariant(dtype):
+    """The hand-over paths (interior point fallback, fp32 refinement list, mpcb_asipm.h /
+    as_ref_kernel_f32) take instances through device-side queues filled by atomics, so their ORDER
+    varies from run to run; an instance's result must not.  On the hard-box draw (many hand-overs):
+    reversing the batch reverses every output bit for bit, and a soak of 12 repeated solves of a
+    4x-tiled batch (several waves racing on the same queues) returns the first solve's bits each
+    time."""
+    from test_oracle_ocp import hard_box_inputs
+    N, B = 18, 192
+    inp = hard_box_inputs(B, N, 11)
+    cast = (lambda a: a.astype(np.float32).astype(np.float64)) if dtype == 'f32' else (lambda a: a)
+    x0, xref, uref, wind = (cast(inp[k]) for k in ('x0', 'xref', 'uref', 'wind'))
+    m = _mpc(N, dtype, True, 4 * B)
+    m.solve(x0, xref, uref, wind=wind)
+    fwd = _outputs(m)
+    r = lambda a: np.ascontiguousarray(a[::-1]) if a.shape[0] == B else a  # noqa: E731
+    m.solve(r(x0), r(xref), r(uref), wind=r(wind))
+    bwd = _outputs(m)
+    for name, a, b in zip(('u0', 'X', 'U', 'status'), fwd, bwd):
+        assert np.array_equal(a, b[::-1]), f'{dtype}: {name} depends on batch order'
+    t = lambda a: np.ascontiguousarray(np.concatenate([a] * 4)) if a.shape[0] == B else a  # noqa: E731
+    x4, xr4, ur4, w4 = t(x0), t(xref), t(uref), t(wind)
+    m.solve(x4, xr4, ur4, wind=w4)
+    first = _outputs(m)
+    for a, b in zip(first, fwd):
+        assert np.array_equal(a[:B], b) and np.array_equal(a[3 * B:], b)
+    for k in range(12):
+        m.solve(x4, xr4, ur4, wind=w4)
+        got = _outputs(m)
+        for name, a, b in zip(('u0', 'X', 'U', 'status'), got, first):
+            assert np.array_equal(a, b), f'{dtype}: soak solve {k}: {name} differs'
+    print(f'{dtype}: order and 12-solve soak bit-identical; status {np.bincount(fwd[3], minlength=5).tolist()}')
+
+
 def test_box_interior_point_from_start_matches_oracle():
     """max_as_iter = 1: every instance whose unconstrained solution leaves the box goes straight to
     the interior point (mpcb.h max_as_iter), on the device as in oracle.ocp.pdas_solve."""

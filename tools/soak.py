@@ -51,6 +51,24 @@ def main():
             n += 1
         bad += diff
         print(f'{name}: {n} repeated solves of {B}, outputs differing from the first: {diff}', flush=True)
+    # the hand-over paths: the hard-box draw (sine references, +-5 N wind) sends about a quarter of
+    # its instances to the interior-point fallback and, in fp32, to the refinement kernel; both
+    # queues are filled by atomics (c4's draws never reach the fallback)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests'))
+    from test_oracle_ocp import hard_box_inputs
+    hb = hard_box_inputs(8192, 18, 11)
+    for dt in ('f64', 'f32'):
+        m = BatchedMPC(MPCConfig(N=18, dtype=dt, lbu=np.zeros(4), ubu=np.full(4, 65.0)), max_batch=8192)
+        m.solve(hb['x0'], hb['xref'], hb['uref'], wind=hb['wind'])
+        ref = outputs(m)
+        t0, n, diff = time.time(), 0, 0
+        while time.time() - t0 < args.seconds / (len(W) + 1):
+            m.solve(hb['x0'], hb['xref'], hb['uref'], wind=hb['wind'])
+            diff += sum(0 if torch.equal(a, b) else 1 for a, b in zip(outputs(m), ref))
+            n += 1
+        bad += diff
+        print(f'hard box {dt}: {n} repeated solves of 8192, outputs differing from the first: {diff}', flush=True)
+        del m
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from sbox_stall_study import draws   # the 17/6 bench draws (tools/bench_full17.py --bounds all)
     x0, xref, uref, p, lbu, ubu, lbx, ubx = draws(60, 1024)
