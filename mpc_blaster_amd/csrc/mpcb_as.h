@@ -686,7 +686,14 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
             lowm |= (M)(uint32_t)ent[w + 1] << 32;
             upm |= (M)(uint32_t)ent[w + 9] << 32;
           }
+          // the set's fixed components at their bounds: an interior-point instance (crossover,
+          // mpcb_asipm.h) left them ~sqrt(mu) inside, and the refinement corrects the free
+          // components only, so those offsets stayed in U (up to 4.8e-4 normwise on the sweep's
+          // wind draws); an active-set instance has them there already
+          for (int k = 0; k < N; ++k)
+            if (((lowm | upm) >> k) & 1u) us0[k * NU + ju] = ((lowm >> k) & 1u) ? lbm : ubm;
         }
+        wave_lds_sync();
       }
     }
   };
@@ -1334,8 +1341,15 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
         // error grows (the hard wind + sine draws: 10-34-pass instances 6e-5 to 1.2e-4 off at an
         // fp32 data sensitivity of 4e-6 to 9e-6; listing from 6 passes on instead -- 4,544 of
         // c4's 65,536 -- took the refinement kernel from 0.33 to 0.47 ms)
+        // ... or whose converged set fixes AS_REF_FIX_NUM / AS_REF_FIX_DEN of the horizon's input
+        // components or more: a strongly constrained QP, on which the fp32 solve's error in the
+        // free components grows (sweep cases 65 / 112, sine references: 4-9 passes, 32-68 % fixed,
+        // 5.1e-5 to 1.4e-4 off; no c4 instance fixes more than 24 %)
+        const int nf = stl ? 0 : Mk::popc(lowm | upm);
+        const bool crowdf = ((bc<NX + 0>(nf) + bc<NX + 1>(nf)) + (bc<NX + 2>(nf) + bc<NX + 3>(nf))) * AS_REF_FIX_DEN >=
+                            AS_REF_FIX_NUM * N * NU;
         const bool lst = cvd && a.as_ref &&
-                         (small || git >= AS_REF_PASSES ||
+                         (small || crowdf || git >= AS_REF_PASSES ||
                           ((bc<NX + 0>(un) | bc<NX + 1>(un)) | (bc<NX + 2>(un) | bc<NX + 3>(un))));
         if (lst) {   // (group-uniform: the row broadcast below has its 16 lanes)
           int t = 0;

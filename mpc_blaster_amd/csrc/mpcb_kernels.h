@@ -137,6 +137,8 @@ constexpr int AS_REF_HDR = 4, AS_REF_W = 24, AS_REF_KC = 20;   // (KC: the resta
 constexpr double AS_REF_U0 = 2.0;
 // ... and converged instances that needed this many active-set passes or more
 constexpr int AS_REF_PASSES = 10;
+// ... and converged instances whose set fixes at least this fraction of the input components
+constexpr int AS_REF_FIX_NUM = 3, AS_REF_FIX_DEN = 10;
 
 template <class T>
 struct SplitArgs {

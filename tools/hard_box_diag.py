@@ -69,7 +69,17 @@ def main():
     print(f'{len(bad)} well-conditioned instances beyond 5e-5 (of {B}); refined {int(refined.sum())}')
     for i in bad[:12]:
         print(f'  {i}: err {e[i]:.2e} (without refinement {e0[i]:.2e}) sens {sens[i]:.1e} qp_stats {qs[i].tolist()} '
-              f'oracle iters {o["iters"][i]} fallback {bool(o["fallback"][i])} refined {bool(refined[i])}')
+              f'(without {res["0"][1][i].tolist()}) oracle iters {o["iters"][i]} fallback {bool(o["fallback"][i])} '
+              f'refined {bool(refined[i])}')
+        # the active sets: device (within 1e-6 of a bound) against the oracle's (1e-9)
+        du, ou = U[i], o['U'][i]
+        dl, dh = du <= 1e-6 * 65, du >= 65 - 1e-6 * 65
+        ol, oh = ou <= 1e-9, ou >= 65 - 1e-9
+        diff = np.argwhere((dl != ol) | (dh != oh))
+        k, m_ = np.unravel_index(np.argmax(np.abs(du - ou)), du.shape)
+        print(f'      active: device {int(dl.sum())}+{int(dh.sum())} oracle {int(ol.sum())}+{int(oh.sum())}; '
+              f'differ at {[(int(a), int(b), round(float(du[a, b]), 5), round(float(ou[a, b]), 5)) for a, b in diff[:6]]}; '
+              f'worst (k={k}, m={m_}) device {du[k, m_]:.6f} oracle {ou[k, m_]:.6f}')
 
 
 if __name__ == '__main__':
