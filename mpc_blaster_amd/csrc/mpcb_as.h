@@ -39,6 +39,16 @@ namespace asq {
 #if defined(MPCB_REF_TRACE) && defined(MPCB_AS_OWNER)
 __device__ int g_ref_trace[128][20];
 #endif
+#if defined(MPCB_REF_STAMPS) && defined(MPCB_AS_OWNER)
+// Diagnostic build only: s_memtime cycles of the refinement's sweeps in workgroup 0 of the
+// refinement kernel, summed over its calls ([0] re-simulation, [1] adjoint for the correction,
+// [2] correction backward, [3] correction forward, [4] deciding adjoint, [5] calls), read by
+// mpcb_debug_ref_stamps() (tools/ref_stamps.py)
+__device__ unsigned long long g_refst[8];
+#define RSTAMP(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); rst[i] += t_ - rst_prev; rst_prev = t_; }
+#else
+#define RSTAMP(i)
+#endif
 #ifdef MPCB_AS_STAMPS
 // Diagnostic build only: per-region s_memtime cycles of workgroup 0, wave-summed over the whole
 // kernel ([0] backward init, [1..3] backward stage parts, [4..6] forward stage parts, [7] forward
@@ -291,6 +301,9 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
     }
   };
   M rd = 0, alo = 0, ahi = 0;   // input lanes: released stages, free components beyond a bound
+#if defined(MPCB_REF_STAMPS) && defined(MPCB_AS_OWNER)
+  unsigned long long rst[8] = {}, rst_prev = __builtin_amdgcn_s_memtime();
+#endif
 
   // (1) the states re-simulated in fp64 from the staged U, x_k into xs
   struct SF { T rv[NVAR]; T yb, gp, rf; };
@@ -324,6 +337,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
       es[N * NX + jx] = (T)(xN - (double)in.xrN[jx]);
     }
   }
+  RSTAMP(0);
   struct SA { T cr[NX]; T rf; };
   int sweeps = 1;   // stage loops run (qp_stats counts each as a forward pass)
   for (int r = 0;; ++r) {
@@ -376,6 +390,11 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
             ahi |= (M)(!lo && !hi && uk > in.ubm + in.tol_u) << k;
           }
         });
+    if (r >= REF_STEPS) {
+      RSTAMP(4);
+    } else {
+      RSTAMP(1);
+    }
     // decided, unless a release is pending and another step is left (wave-uniform)
     if (r >= REF_STEPS) {
       if (r == REF_STEPS_MAX || !__builtin_amdgcn_ballot_w64(ver && rd != 0)) break;
@@ -461,6 +480,7 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
           pc = stl ? pn : T(0);
           if (!stl && ver) dks[k * NU + ju] = sel<NU>(kff, ju);
         });
+    RSTAMP(2);
     // (3) the correction's forward pass with the stored gains (KR2), fused with the next
     // re-simulation: u_k += K_k (x_k - x_k^old) + d_k (input lanes), then x_{k+1} in fp64 from the
     // refined u (state lanes; x_k^old: the previous re-simulation in xs)
@@ -507,7 +527,14 @@ __device__ __forceinline__ RefOut<W32> refine_verify(const RefIn<W32>& in) {
       xs[N * NX + jx] = (T)xN;
       es[N * NX + jx] = (T)(xN - (double)in.xrN[jx]);
     }
+    RSTAMP(3);
   }
+#if defined(MPCB_REF_STAMPS) && defined(MPCB_AS_OWNER)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int i_ = 0; i_ < 5; ++i_) g_refst[i_] += rst[i_];
+    g_refst[5] += 1;
+  }
+#endif
   return RefOut<W32>{rd, alo, ahi, sweeps};
 }
 

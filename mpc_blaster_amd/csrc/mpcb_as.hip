@@ -145,6 +145,15 @@ template hipError_t launch_as<float>(const SplitArgs<float>&, hipStream_t);
 
 }  // namespace mpcb
 
+#ifdef MPCB_REF_STAMPS
+extern "C" int mpcb_debug_ref_stamps(unsigned long long* out, int reset) {
+  if (reset) {
+    const unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mpcb::asq::g_refst), z, sizeof(z)) == hipSuccess ? 0 : -2;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_refst), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef MPCB_REF_TRACE
 extern "C" int mpcb_debug_ref_trace(int* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcb::asq::g_ref_trace), sizeof(int) * 128 * 20) == hipSuccess ? 0 : -2;
