@@ -1209,7 +1209,7 @@ __device__ __forceinline__ void as_body(const SplitArgs<T>& args) {
     //          cycled), and the Kim-Park update below proceeds on them.
     // The active-set kernel lists the instances whose converged set has an undecided multiplier
     // (as_ref_put); the refinement kernel restores each set, redoes its final forward pass and runs
-    // every further pass this way.  Each refinement is counted as six forward passes in qp_stats.
+    // every further pass this way.  Each refinement is counted as five forward passes (its sweeps) in qp_stats.
     // The output X of a refined instance is the fp64 re-simulation of its U.
     // Oracle: oracle.ocp.pdas_solve (the exact-arithmetic active set).
     if constexpr (VER) {
