@@ -821,7 +821,7 @@ def fp32_sensitivity(o, x0, xref, uref, spec: OcpSpec, trials: int = 2, rel: flo
     An fp32 solver's own linearisation carries at least this much error, so an instance that moves
     by more than a parity bound here cannot be held to it by ANY fp32 computation: the sweeps hold
     such instances (counted and printed) to the QP's optimal objective instead
-    (tests/test_gpu_fuzz.py).  On c4's draws the move is ~1e-7; on strongly constrained short
+    (tests/test_gpu_fuzz.py).  On c4's draws the move is ~1e-6 (tests/test_oracle_sensitivity.py); on strongly constrained short
     horizons (sweep cases 33 / 67 / 158: N = 2, 6, 4, wind) up to 2e-4."""
     B = x0.shape[0]
     N = spec.N
